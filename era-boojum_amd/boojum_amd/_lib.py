@@ -1,0 +1,76 @@
+"""ctypes binding of libboojum_mi355x.so (include/boojum_mi355x.h).
+
+This is the product's only route to compute: there is no CPU fallback.  If the
+library is missing, importing a compute entry point raises immediately.
+"""
+import ctypes
+import os
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(_HERE, "libboojum_mi355x.so")
+
+_u64 = ctypes.c_uint64
+_u32 = ctypes.c_uint32
+_sz = ctypes.c_size_t
+_int = ctypes.c_int
+_vp = ctypes.c_void_p
+_u64p = ctypes.POINTER(ctypes.c_uint64)
+
+# name -> argtypes (restype int unless noted).  Every symbol the header declares.
+SIGNATURES = {
+    "bj_last_error": ([], ctypes.c_char_p),
+    "bj_abi_version": ([], _u32),
+    "bj_prepare": ([_u32], _int),
+    "bj_precompute_twiddles_d": ([_u32, _int, _vp, _vp], _int),
+    "bj_precompute_twiddles_h": ([_u32, _int, _u64p], _int),
+    "bj_distribute_powers_d": ([_vp, _u32, _sz, _u32, _u64, _vp], _int),
+    "bj_distribute_powers_h": ([_u64p, _sz, _u64], _int),
+    "bj_fft_natural_to_bitreversed_d": ([_vp, _u32, _sz, _u32, _u64, _vp, _vp], _int),
+    "bj_fft_natural_to_bitreversed_h": ([_u64p, _sz, _u64], _int),
+    "bj_ifft_natural_to_natural_d": ([_vp, _u32, _sz, _u32, _u64, _vp, _vp], _int),
+    "bj_ifft_natural_to_natural_h": ([_u64p, _sz, _u64], _int),
+    "bj_lde_d": ([_vp, _u32, _sz, _u32, _u32, _vp, _vp, _vp], _int),
+    "bj_monomials_to_lde_d": ([_vp, _u32, _sz, _u32, _u32, _vp, _vp], _int),
+    "bj_poseidon2_permute_d": ([_vp, _sz, _vp], _int),
+    "bj_poseidon2_permute_h": ([_u64p], _int),
+    "bj_hash_into_leaf_h": ([_u64p, _sz, _u64p], _int),
+    "bj_hash_into_node_h": ([_u64p, _u64p, _u64p], _int),
+    "bj_merkle_leaves_d": ([_vp, _u32, _sz, _sz, _vp, _vp], _int),
+    "bj_merkle_nodes_d": ([_vp, _sz, _u32, _vp, _vp], _int),
+    "bj_lde_commit_d": ([_vp, _u32, _sz, _u32, _u32, _u32, _vp, _vp, _vp, _vp, _u64p, _vp], _int),
+    "bj_lde_commit_h": ([_u64p, _u32, _u32, _u32, _u32, _u64p, _u64p, _u64p, _u64p], _int),
+    "bj_fill_synthetic_d": ([_vp, _u32, _sz, _u32, _u64, _u64, _vp], _int),
+}
+
+_LIB = None
+
+
+class BoojumError(RuntimeError):
+    pass
+
+
+def load():
+    """Load the HIP library (raises if it is not built: no fallback path exists)."""
+    global _LIB
+    if _LIB is None:
+        if not os.path.exists(LIB_PATH):
+            raise BoojumError(
+                "libboojum_mi355x.so not found at %s -- build it with "
+                "`make -C era-boojum_amd` (or __graft_entry__.build())" % LIB_PATH)
+        L = ctypes.CDLL(LIB_PATH)
+        for name, (args, res) in SIGNATURES.items():
+            fn = getattr(L, name)
+            fn.argtypes = args
+            fn.restype = res
+        _LIB = L
+    return _LIB
+
+
+def check(rc, what=""):
+    if rc != 0:
+        msg = load().bj_last_error()
+        raise BoojumError("%s failed (%d): %s" % (what, rc, msg.decode() if msg else ""))
+
+
+def call(name, *args):
+    check(getattr(load(), name)(*args), name)

@@ -1,0 +1,66 @@
+"""The witness-commitment hot path as one batched call.
+
+`witness_commit` = prover.rs:313-353 with fri_lde_factor == lde degree: LDE of every
+column (transform_raw_storages_to_lde), MerkleTreeWithCap::construct over the n*D rows,
+get_cap.  `CommitWorkspace` preallocates every HBM buffer once so repeated commits
+(the bench loop, a prover running many circuits) never allocate.
+"""
+import torch
+
+from ._lib import call
+from .field import col_view, stream_of
+
+
+def _log2(n):
+    if n <= 0 or n & (n - 1):
+        raise ValueError("size must be a power of two, got %d" % n)
+    return n.bit_length() - 1
+
+
+class CommitWorkspace:
+    """HBM buffers for a commit of n_cols x 2^log_n at LDE 2^log_lde, cap cap_size.
+
+    Sizes (bytes): monomials 8*C*n, lde 8*C*n*D, leaves 32*n*D, nodes 32*(n*D - cap)."""
+
+    def __init__(self, n_cols, log_n, log_lde, cap_size, device="cuda"):
+        n, d = 1 << log_n, 1 << log_lde
+        nl = n * d
+        _log2(cap_size)
+        if nl <= cap_size:
+            raise ValueError("tree size must exceed cap size")
+        self.n_cols, self.log_n, self.log_lde, self.cap_size = n_cols, log_n, log_lde, cap_size
+        self.monomials = torch.empty((n_cols, n), dtype=torch.int64, device=device)
+        self.lde = torch.empty((n_cols, d, n), dtype=torch.int64, device=device)
+        self.leaves = torch.empty((nl, 4), dtype=torch.int64, device=device)
+        self.nodes = torch.empty((nl - cap_size, 4), dtype=torch.int64, device=device)
+        call("bj_prepare", log_n)
+
+    @property
+    def cap(self):
+        return self.nodes[-self.cap_size:]
+
+    def tree(self):
+        from .merkle import MerkleTreeWithCap
+        return MerkleTreeWithCap(self.cap_size, self.leaves, self.nodes)
+
+
+def witness_commit(trace, lde_degree, cap_size, workspace=None):
+    """Commit a (C, n) int64 CUDA trace tensor.  Returns the workspace holding
+    monomials, lde (C, D, n), leaves, nodes and cap (all on device, canonical).
+    Asynchronous on the current stream."""
+    v, c, n, stride = col_view(trace)
+    log_n, log_d = _log2(n), _log2(lde_degree)
+    ws = workspace or CommitWorkspace(c, log_n, log_d, cap_size, device=v.device)
+    if (ws.n_cols, ws.log_n, ws.log_lde, ws.cap_size) != (c, log_n, log_d, cap_size):
+        raise ValueError("workspace shape does not match the trace")
+    call("bj_lde_commit_d", v.data_ptr(), c, stride, log_n, log_d, cap_size, ws.monomials.data_ptr(),
+         ws.lde.data_ptr(), ws.leaves.data_ptr(), ws.nodes.data_ptr(), None, stream_of(v))
+    return ws
+
+
+def synthetic_trace(n_cols, log_n, seed=42, first_col=0, device="cuda", out=None):
+    """Device-generated synthetic trace: splitmix64(seed + c*n + r) mod p."""
+    n = 1 << log_n
+    t = out if out is not None else torch.empty((n_cols, n), dtype=torch.int64, device=device)
+    call("bj_fill_synthetic_d", t.data_ptr(), n_cols, n, log_n, seed, first_col, stream_of(t))
+    return t

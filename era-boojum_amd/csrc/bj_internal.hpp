@@ -1,0 +1,31 @@
+// Internal launcher declarations shared by the .hip translation units.
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+#include <stddef.h>
+
+namespace bj {
+
+hipError_t launch_ntt_nb(uint64_t* dst, size_t dst_stride, const uint64_t* src, size_t src_stride,
+                         uint32_t n_cols, uint32_t log_n, const uint64_t* tw, const uint64_t* pw_lo,
+                         const uint64_t* pw_hi, bool canon_out, hipStream_t st);
+hipError_t launch_bitrev_scale(uint64_t* dst, size_t dst_stride, const uint64_t* src, size_t src_stride,
+                               uint32_t n_cols, uint32_t log_n, uint64_t scale, hipStream_t st);
+hipError_t launch_twiddles(uint64_t* out, uint32_t log_n, bool inverse, hipStream_t st);
+hipError_t launch_power_tables(uint64_t* lo, uint64_t* hi, uint32_t log_n, uint64_t e, uint64_t scale,
+                               hipStream_t st);
+hipError_t launch_distribute(uint64_t* cols, size_t col_stride, uint32_t n_cols, uint32_t log_n,
+                             const uint64_t* lo, const uint64_t* hi, hipStream_t st);
+
+hipError_t launch_leaves(const uint64_t* src, size_t col_stride, uint32_t n_cols, size_t n_leaves, uint64_t* out,
+                         hipStream_t st);
+hipError_t launch_nodes(const uint64_t* leaves, size_t n_leaves, uint32_t cap_size, uint64_t* nodes,
+                        hipStream_t st);
+hipError_t launch_permute(uint64_t* states, size_t count, hipStream_t st);
+hipError_t launch_synthetic(uint64_t* dst, size_t col_stride, uint32_t n_cols, uint32_t log_n, uint64_t seed,
+                            uint64_t col0, hipStream_t st);
+
+// power table sizes for a column of 2^log_n: lo 4096, hi max(1, n / 4096)
+inline size_t pw_hi_len(uint32_t log_n) { return log_n > 12 ? ((size_t)1 << (log_n - 12)) : 1; }
+
+}  // namespace bj

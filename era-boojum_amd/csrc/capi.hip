@@ -1,0 +1,376 @@
+// C ABI of the MI355X witness-commitment path (include/boojum_mi355x.h).
+// Host-side orchestration only: argument checks (the reference's asserts), the per-device
+// twiddle / coset-power cache, and the kernel launch sequences for each entry point.
+#include <hip/hip_runtime.h>
+#include <map>
+#include <mutex>
+#include <string>
+#include <tuple>
+#include <vector>
+#include <cstring>
+#include <cstdio>
+
+#include "../../include/boojum_mi355x.h"
+#include "gl.hpp"
+#include "bj_internal.hpp"
+
+namespace {
+
+thread_local std::string g_err;
+
+int fail(int code, const std::string& msg) {
+    g_err = msg;
+    return code;
+}
+
+int hip_fail(hipError_t e, const char* what) {
+    return fail(BJ_EHIP, std::string(what) + ": " + hipGetErrorString(e));
+}
+
+#define HIP_TRY(expr, what)                       \
+    do {                                          \
+        hipError_t _e = (expr);                   \
+        if (_e != hipSuccess) return hip_fail(_e, what); \
+    } while (0)
+
+inline hipStream_t S(void* s) { return reinterpret_cast<hipStream_t>(s); }
+
+// ------------------------------------------------------------ device cache
+// Twiddles per (device, log_n, inverse); power tables per (device, log_n, e, scale).
+// Entries are computed synchronously on a private stream when first inserted, so any
+// caller stream can use them afterwards without ordering concerns; never freed (they are
+// small: n/2 u64 per twiddle table, 4096 + n/4096 u64 per power table).
+struct Cache {
+    std::mutex mu;
+    std::map<std::tuple<int, uint32_t, int>, uint64_t*> tw;
+    std::map<std::tuple<int, uint32_t, uint64_t, uint64_t>, std::pair<uint64_t*, uint64_t*>> pw;
+};
+Cache& cache() {
+    static Cache* c = new Cache();
+    return *c;
+}
+
+int get_twiddles(uint32_t log_n, bool inverse, const uint64_t** out) {
+    int dev = 0;
+    HIP_TRY(hipGetDevice(&dev), "hipGetDevice");
+    Cache& c = cache();
+    std::lock_guard<std::mutex> lk(c.mu);
+    auto key = std::make_tuple(dev, log_n, inverse ? 1 : 0);
+    auto it = c.tw.find(key);
+    if (it != c.tw.end()) { *out = it->second; return BJ_OK; }
+    size_t half = log_n ? ((size_t)1 << (log_n - 1)) : 1;
+    uint64_t* p = nullptr;
+    HIP_TRY(hipMalloc(&p, half * sizeof(uint64_t)), "hipMalloc(twiddles)");
+    hipStream_t st;
+    HIP_TRY(hipStreamCreateWithFlags(&st, hipStreamNonBlocking), "hipStreamCreate");
+    hipError_t e = bj::launch_twiddles(p, log_n, inverse, st);
+    if (e == hipSuccess) e = hipStreamSynchronize(st);
+    (void)hipStreamDestroy(st);
+    if (e != hipSuccess) { (void)hipFree(p); return hip_fail(e, "twiddles"); }
+    c.tw[key] = p;
+    *out = p;
+    return BJ_OK;
+}
+
+int get_powers(uint32_t log_n, uint64_t e_, uint64_t scale, const uint64_t** lo, const uint64_t** hi) {
+    int dev = 0;
+    HIP_TRY(hipGetDevice(&dev), "hipGetDevice");
+    const uint64_t e = gl::canon(e_);
+    Cache& c = cache();
+    std::lock_guard<std::mutex> lk(c.mu);
+    auto key = std::make_tuple(dev, log_n, e, gl::canon(scale));
+    auto it = c.pw.find(key);
+    if (it != c.pw.end()) { *lo = it->second.first; *hi = it->second.second; return BJ_OK; }
+    size_t nhi = bj::pw_hi_len(log_n);
+    uint64_t* p = nullptr;
+    HIP_TRY(hipMalloc(&p, (4096 + nhi) * sizeof(uint64_t)), "hipMalloc(powers)");
+    hipStream_t st;
+    HIP_TRY(hipStreamCreateWithFlags(&st, hipStreamNonBlocking), "hipStreamCreate");
+    hipError_t er = bj::launch_power_tables(p, p + 4096, log_n, e, scale, st);
+    if (er == hipSuccess) er = hipStreamSynchronize(st);
+    (void)hipStreamDestroy(st);
+    if (er != hipSuccess) { (void)hipFree(p); return hip_fail(er, "power tables"); }
+    c.pw[key] = {p, p + 4096};
+    *lo = p;
+    *hi = p + 4096;
+    return BJ_OK;
+}
+
+inline bool is_pow2(size_t x) { return x && !(x & (x - 1)); }
+
+int log2_exact(size_t len, uint32_t* out) {
+    if (!is_pow2(len)) return fail(BJ_EINVAL, "length must be a power of two");
+    uint32_t l = 0;
+    while (((size_t)1 << l) < len) l++;
+    *out = l;
+    return BJ_OK;
+}
+
+int check_log_n(uint32_t log_n) {
+    if (log_n > 32) return fail(BJ_EINVAL, "log_n exceeds the 2-adicity (32) of the field");
+    return BJ_OK;
+}
+
+// LDE coset shifts 7 * w_{nD}^{bitrev_{log D}(i)} (utils.rs:334-347, 370-373).
+uint64_t lde_coset(uint32_t log_n, uint32_t log_d, uint32_t i) {
+    uint64_t g = gl::domain_generator(log_n + log_d);
+    return gl::canon(gl::mul(gl::pow(g, gl::bitrev32(i, log_d)), gl::GENERATOR));
+}
+
+// Device buffer RAII for the *_h entry points.
+struct DBuf {
+    uint64_t* p = nullptr;
+    ~DBuf() { if (p) (void)hipFree(p); }
+};
+
+}  // namespace
+
+extern "C" {
+
+const char* bj_last_error(void) { return g_err.c_str(); }
+uint32_t bj_abi_version(void) { return (1u << 16) | 0u; }
+
+int bj_prepare(uint32_t log_n) {
+    if (int r = check_log_n(log_n)) return r;
+    const uint64_t* t;
+    if (int r = get_twiddles(log_n, false, &t)) return r;
+    if (int r = get_twiddles(log_n, true, &t)) return r;
+    return BJ_OK;
+}
+
+int bj_precompute_twiddles_d(uint32_t log_n, int inverse, uint64_t* out_d, void* stream) {
+    if (int r = check_log_n(log_n)) return r;
+    if (log_n == 0) return fail(BJ_EINVAL, "twiddles need n >= 2");
+    HIP_TRY(bj::launch_twiddles(out_d, log_n, inverse != 0, S(stream)), "twiddles");
+    return BJ_OK;
+}
+
+int bj_precompute_twiddles_h(uint32_t log_n, int inverse, uint64_t* out_h) {
+    if (int r = check_log_n(log_n)) return r;
+    if (log_n == 0) return fail(BJ_EINVAL, "twiddles need n >= 2");
+    const uint64_t* t;
+    if (int r = get_twiddles(log_n, inverse != 0, &t)) return r;
+    HIP_TRY(hipMemcpy(out_h, t, ((size_t)1 << (log_n - 1)) * 8, hipMemcpyDeviceToHost), "memcpy");
+    return BJ_OK;
+}
+
+int bj_distribute_powers_d(uint64_t* cols, uint32_t n_cols, size_t col_stride, uint32_t log_n, uint64_t element,
+                           void* stream) {
+    if (int r = check_log_n(log_n)) return r;
+    const uint64_t *lo, *hi;
+    if (int r = get_powers(log_n, element, 1, &lo, &hi)) return r;
+    HIP_TRY(bj::launch_distribute(cols, col_stride, n_cols, log_n, lo, hi, S(stream)), "distribute");
+    return BJ_OK;
+}
+
+int bj_fft_natural_to_bitreversed_d(uint64_t* cols, uint32_t n_cols, size_t col_stride, uint32_t log_n,
+                                    uint64_t coset, const uint64_t* twiddles_d, void* stream) {
+    if (int r = check_log_n(log_n)) return r;
+    const uint64_t* tw = twiddles_d;
+    if (!tw && log_n > 0)
+        if (int r = get_twiddles(log_n, false, &tw)) return r;
+    const uint64_t *lo = nullptr, *hi = nullptr;
+    if (gl::canon(coset) != 1)
+        if (int r = get_powers(log_n, coset, 1, &lo, &hi)) return r;
+    HIP_TRY(bj::launch_ntt_nb(cols, col_stride, cols, col_stride, n_cols, log_n, tw, lo, hi, true, S(stream)),
+            "fft");
+    return BJ_OK;
+}
+
+int bj_ifft_natural_to_natural_d(uint64_t* cols, uint32_t n_cols, size_t col_stride, uint32_t log_n,
+                                 uint64_t coset, const uint64_t* inv_twiddles_d, void* stream) {
+    if (int r = check_log_n(log_n)) return r;
+    if (n_cols == 0) return BJ_OK;
+    const uint64_t* tw = inv_twiddles_d;
+    if (!tw && log_n > 0)
+        if (int r = get_twiddles(log_n, true, &tw)) return r;
+    const size_t n = (size_t)1 << log_n;
+    // The bit-reversal is out of place; stage through a temporary of the same shape.
+    uint64_t* tmp = nullptr;
+    HIP_TRY(hipMallocAsync((void**)&tmp, n * n_cols * 8, S(stream)), "hipMallocAsync");
+    hipError_t e = bj::launch_ntt_nb(tmp, n, cols, col_stride, n_cols, log_n, tw, nullptr, nullptr, false, S(stream));
+    const uint64_t n_inv = log_n ? gl::canon(gl::inv((uint64_t)n)) : 1;
+    if (e == hipSuccess) e = bj::launch_bitrev_scale(cols, col_stride, tmp, n, n_cols, log_n, n_inv, S(stream));
+    hipError_t e2 = hipFreeAsync(tmp, S(stream));
+    if (e != hipSuccess) return hip_fail(e, "ifft");
+    if (e2 != hipSuccess) return hip_fail(e2, "hipFreeAsync");
+    if (gl::canon(coset) != 1) {
+        const uint64_t *lo, *hi;
+        if (int r = get_powers(log_n, gl::inv(gl::canon(coset)), 1, &lo, &hi)) return r;
+        HIP_TRY(bj::launch_distribute(cols, col_stride, n_cols, log_n, lo, hi, S(stream)), "distribute");
+    }
+    return BJ_OK;
+}
+
+int bj_monomials_to_lde_d(const uint64_t* monomials, uint32_t n_cols, size_t mono_stride, uint32_t log_n,
+                          uint32_t log_lde, uint64_t* lde, void* stream) {
+    if (int r = check_log_n(log_n + log_lde)) return r;
+    if (log_lde == 0) return fail(BJ_EINVAL, "lde degree must be > 1 (utils.rs:283)");
+    const size_t n = (size_t)1 << log_n;
+    const uint32_t D = 1u << log_lde;
+    const uint64_t* tw = nullptr;
+    if (log_n > 0)
+        if (int r = get_twiddles(log_n, false, &tw)) return r;
+    for (uint32_t i = 0; i < D; i++) {
+        const uint64_t *lo, *hi;
+        if (int r = get_powers(log_n, lde_coset(log_n, log_lde, i), 1, &lo, &hi)) return r;
+        HIP_TRY(bj::launch_ntt_nb(lde + (size_t)i * n, (size_t)D * n, monomials, mono_stride, n_cols, log_n, tw, lo,
+                                  hi, true, S(stream)),
+                "coset fft");
+    }
+    return BJ_OK;
+}
+
+int bj_lde_d(const uint64_t* trace, uint32_t n_cols, size_t trace_stride, uint32_t log_n, uint32_t log_lde,
+             uint64_t* monomials, uint64_t* lde, void* stream) {
+    if (int r = check_log_n(log_n + log_lde)) return r;
+    if (log_lde == 0) return fail(BJ_EINVAL, "lde degree must be > 1 (utils.rs:283)");
+    if (n_cols == 0) return BJ_OK;
+    const size_t n = (size_t)1 << log_n;
+    const uint32_t D = 1u << log_lde;
+    const uint64_t* itw = nullptr;
+    if (log_n > 0)
+        if (int r = get_twiddles(log_n, true, &itw)) return r;
+    // iFFT (utils.rs:295-304): CT with inverse twiddles into coset slot 0 of the LDE buffer
+    // (free scratch at this point), then bit-reverse * n^-1 into the monomial buffer.
+    HIP_TRY(bj::launch_ntt_nb(lde, (size_t)D * n, trace, trace_stride, n_cols, log_n, itw, nullptr, nullptr, false,
+                              S(stream)),
+            "ifft");
+    const uint64_t n_inv = log_n ? gl::canon(gl::inv((uint64_t)n)) : 1;
+    HIP_TRY(bj::launch_bitrev_scale(monomials, n, lde, (size_t)D * n, n_cols, log_n, n_inv, S(stream)), "bitrev");
+    return bj_monomials_to_lde_d(monomials, n_cols, n, log_n, log_lde, lde, stream);
+}
+
+int bj_fill_synthetic_d(uint64_t* dst, uint32_t n_cols, size_t col_stride, uint32_t log_n, uint64_t seed,
+                        uint64_t first_col, void* stream) {
+    if (int r = check_log_n(log_n)) return r;
+    HIP_TRY(bj::launch_synthetic(dst, col_stride, n_cols, log_n, seed, first_col, S(stream)), "synthetic");
+    return BJ_OK;
+}
+
+int bj_poseidon2_permute_d(uint64_t* states, size_t count, void* stream) {
+    HIP_TRY(bj::launch_permute(states, count, S(stream)), "permute");
+    return BJ_OK;
+}
+
+int bj_merkle_leaves_d(const uint64_t* src, uint32_t n_cols, size_t col_stride, size_t n_leaves, uint64_t* leaves,
+                       void* stream) {
+    HIP_TRY(bj::launch_leaves(src, col_stride, n_cols, n_leaves, leaves, S(stream)), "leaves");
+    return BJ_OK;
+}
+
+int bj_merkle_nodes_d(const uint64_t* leaves, size_t n_leaves, uint32_t cap_size, uint64_t* nodes, void* stream) {
+    if (!is_pow2(n_leaves) || !is_pow2(cap_size) || n_leaves <= cap_size)
+        return fail(BJ_EINVAL, "need power-of-two n_leaves > cap_size (merkle_tree.rs:83-96)");
+    HIP_TRY(bj::launch_nodes(leaves, n_leaves, cap_size, nodes, S(stream)), "nodes");
+    return BJ_OK;
+}
+
+int bj_lde_commit_d(const uint64_t* trace, uint32_t n_cols, size_t trace_stride, uint32_t log_n, uint32_t log_lde,
+                    uint32_t cap_size, uint64_t* monomials, uint64_t* lde, uint64_t* leaves, uint64_t* nodes,
+                    uint64_t* cap_h, void* stream) {
+    const size_t nl = (size_t)1 << (log_n + log_lde);
+    if (!is_pow2(cap_size) || nl <= cap_size)
+        return fail(BJ_EINVAL, "need power-of-two cap_size < n * D (merkle_tree.rs:83-96)");
+    if (int r = bj_lde_d(trace, n_cols, trace_stride, log_n, log_lde, monomials, lde, stream)) return r;
+    if (int r = bj_merkle_leaves_d(lde, n_cols, nl, nl, leaves, stream)) return r;
+    if (int r = bj_merkle_nodes_d(leaves, nl, cap_size, nodes, stream)) return r;
+    if (cap_h) {
+        HIP_TRY(hipMemcpyAsync(cap_h, nodes + 4 * (nl - 2 * (size_t)cap_size), (size_t)cap_size * 32,
+                               hipMemcpyDeviceToHost, S(stream)),
+                "memcpy cap");
+        HIP_TRY(hipStreamSynchronize(S(stream)), "sync");
+    }
+    return BJ_OK;
+}
+
+// --------------------------------------------------------- host-pointer seam
+
+int bj_distribute_powers_h(uint64_t* col, size_t len, uint64_t element) {
+    uint32_t log_n;
+    if (int r = log2_exact(len, &log_n)) return r;
+    DBuf d;
+    HIP_TRY(hipMalloc(&d.p, len * 8), "hipMalloc");
+    HIP_TRY(hipMemcpy(d.p, col, len * 8, hipMemcpyHostToDevice), "memcpy");
+    if (int r = bj_distribute_powers_d(d.p, 1, len, log_n, element, nullptr)) return r;
+    HIP_TRY(hipMemcpy(col, d.p, len * 8, hipMemcpyDeviceToHost), "memcpy");
+    return BJ_OK;
+}
+
+int bj_fft_natural_to_bitreversed_h(uint64_t* col, size_t len, uint64_t coset) {
+    uint32_t log_n;
+    if (int r = log2_exact(len, &log_n)) return r;
+    DBuf d;
+    HIP_TRY(hipMalloc(&d.p, len * 8), "hipMalloc");
+    HIP_TRY(hipMemcpy(d.p, col, len * 8, hipMemcpyHostToDevice), "memcpy");
+    if (int r = bj_fft_natural_to_bitreversed_d(d.p, 1, len, log_n, coset, nullptr, nullptr)) return r;
+    HIP_TRY(hipMemcpy(col, d.p, len * 8, hipMemcpyDeviceToHost), "memcpy");
+    return BJ_OK;
+}
+
+int bj_ifft_natural_to_natural_h(uint64_t* col, size_t len, uint64_t coset) {
+    uint32_t log_n;
+    if (int r = log2_exact(len, &log_n)) return r;
+    DBuf d;
+    HIP_TRY(hipMalloc(&d.p, len * 8), "hipMalloc");
+    HIP_TRY(hipMemcpy(d.p, col, len * 8, hipMemcpyHostToDevice), "memcpy");
+    if (int r = bj_ifft_natural_to_natural_d(d.p, 1, len, log_n, coset, nullptr, nullptr)) return r;
+    HIP_TRY(hipMemcpy(col, d.p, len * 8, hipMemcpyDeviceToHost), "memcpy");
+    return BJ_OK;
+}
+
+int bj_poseidon2_permute_h(uint64_t* state12) {
+    DBuf d;
+    HIP_TRY(hipMalloc(&d.p, 96), "hipMalloc");
+    HIP_TRY(hipMemcpy(d.p, state12, 96, hipMemcpyHostToDevice), "memcpy");
+    if (int r = bj_poseidon2_permute_d(d.p, 1, nullptr)) return r;
+    HIP_TRY(hipMemcpy(state12, d.p, 96, hipMemcpyDeviceToHost), "memcpy");
+    return BJ_OK;
+}
+
+int bj_hash_into_leaf_h(const uint64_t* elems, size_t n_elems, uint64_t* out4) {
+    DBuf d, o;
+    HIP_TRY(hipMalloc(&d.p, (n_elems ? n_elems : 1) * 8), "hipMalloc");
+    HIP_TRY(hipMalloc(&o.p, 32), "hipMalloc");
+    if (n_elems) HIP_TRY(hipMemcpy(d.p, elems, n_elems * 8, hipMemcpyHostToDevice), "memcpy");
+    if (int r = bj_merkle_leaves_d(d.p, (uint32_t)n_elems, 1, 1, o.p, nullptr)) return r;
+    HIP_TRY(hipMemcpy(out4, o.p, 32, hipMemcpyDeviceToHost), "memcpy");
+    return BJ_OK;
+}
+
+int bj_hash_into_node_h(const uint64_t* left4, const uint64_t* right4, uint64_t* out4) {
+    DBuf d;
+    HIP_TRY(hipMalloc(&d.p, 96), "hipMalloc");
+    HIP_TRY(hipMemcpy(d.p, left4, 32, hipMemcpyHostToDevice), "memcpy");
+    HIP_TRY(hipMemcpy(d.p + 4, right4, 32, hipMemcpyHostToDevice), "memcpy");
+    if (int r = bj_merkle_nodes_d(d.p, 2, 1, d.p + 8, nullptr)) return r;
+    HIP_TRY(hipMemcpy(out4, d.p + 8, 32, hipMemcpyDeviceToHost), "memcpy");
+    return BJ_OK;
+}
+
+int bj_lde_commit_h(const uint64_t* trace_h, uint32_t n_cols, uint32_t log_n, uint32_t log_lde, uint32_t cap_size,
+                    uint64_t* lde_h, uint64_t* leaves_h, uint64_t* nodes_h, uint64_t* cap_h) {
+    if (int r = check_log_n(log_n + log_lde)) return r;
+    const size_t n = (size_t)1 << log_n, nl = n << log_lde;
+    if (!is_pow2(cap_size) || nl <= cap_size) return fail(BJ_EINVAL, "need power-of-two cap_size < n * D");
+    DBuf tr, mono, lde, lv, nd;
+    const size_t tn = n * n_cols;
+    HIP_TRY(hipMalloc(&tr.p, (tn ? tn : 1) * 8), "hipMalloc");
+    HIP_TRY(hipMalloc(&mono.p, (tn ? tn : 1) * 8), "hipMalloc");
+    HIP_TRY(hipMalloc(&lde.p, (tn ? tn << log_lde : 1) * 8), "hipMalloc");
+    HIP_TRY(hipMalloc(&lv.p, nl * 32), "hipMalloc");
+    HIP_TRY(hipMalloc(&nd.p, (nl - cap_size) * 32), "hipMalloc");
+    if (tn) HIP_TRY(hipMemcpy(tr.p, trace_h, tn * 8, hipMemcpyHostToDevice), "memcpy");
+    if (int r = bj_lde_commit_d(tr.p, n_cols, n, log_n, log_lde, cap_size, mono.p, lde.p, lv.p, nd.p, nullptr, nullptr))
+        return r;
+    HIP_TRY(hipDeviceSynchronize(), "sync");
+    if (lde_h && tn) HIP_TRY(hipMemcpy(lde_h, lde.p, (tn << log_lde) * 8, hipMemcpyDeviceToHost), "memcpy");
+    if (leaves_h) HIP_TRY(hipMemcpy(leaves_h, lv.p, nl * 32, hipMemcpyDeviceToHost), "memcpy");
+    if (nodes_h) HIP_TRY(hipMemcpy(nodes_h, nd.p, (nl - cap_size) * 32, hipMemcpyDeviceToHost), "memcpy");
+    if (cap_h)
+        HIP_TRY(hipMemcpy(cap_h, nd.p + 4 * (nl - 2 * (size_t)cap_size), (size_t)cap_size * 32, hipMemcpyDeviceToHost),
+                "memcpy");
+    return BJ_OK;
+}
+
+}  // extern "C"

@@ -1,0 +1,154 @@
+// Poseidon2 leaf / node hashing kernels (gfx950).
+//
+// Leaf: MerkleTreeWithCap::construct (cs/oracle/merkle_tree.rs:78-172) hashes, for each
+// flat leaf index L = coset * n + row, the elements src[0][L], ..., src[C-1][L] with the
+// Overwrite sponge (algebraic_props/sponge.rs:224-323): every 8 elements overwrite
+// state[0..8] and permute; a partial last group is zero-padded to 8 and permuted; the
+// digest is state[0..4].  One leaf per lane, state in VGPRs; lanes read consecutive L
+// of one column at a time, so each wave load is 512 contiguous bytes.
+//
+// Node: hash_into_node (cs/oracle/mod.rs:162-168) = permute([l, r, 0,0,0,0])[0..4], one
+// node per lane, level by level (continue_from_leaf_hashes, merkle_tree.rs:388-449);
+// the last levels (<= 2048 nodes) run in one workgroup through LDS.
+#include <hip/hip_runtime.h>
+#include "gl.hpp"
+#include "poseidon2.hpp"
+#include "bj_internal.hpp"
+
+namespace bj {
+
+constexpr int LEAF_THREADS = 256;
+
+__global__ __launch_bounds__(LEAF_THREADS) void leaf_hash_kernel(const uint64_t* __restrict__ src,
+                                                                 size_t col_stride, uint32_t n_cols,
+                                                                 size_t n_leaves, uint64_t* __restrict__ out) {
+    const size_t L = blockIdx.x * (size_t)LEAF_THREADS + threadIdx.x;
+    if (L >= n_leaves) return;
+    const uint64_t* p = src + L;
+    uint64_t s[12];
+#pragma unroll
+    for (int i = 0; i < 12; i++) s[i] = 0;
+    const uint32_t full = n_cols >> 3;
+    const uint32_t rem = n_cols & 7;
+    // software prefetch: the next group's 8 loads are issued before this group's permute
+    uint64_t nxt[8];
+    if (full > 0) {
+#pragma unroll
+        for (int i = 0; i < 8; i++) nxt[i] = p[(size_t)i * col_stride];
+    }
+    for (uint32_t g = 0; g < full; g++) {
+#pragma unroll
+        for (int i = 0; i < 8; i++) s[i] = nxt[i];
+        if (g + 1 < full) {
+            const uint64_t* q = p + (size_t)(g + 1) * 8 * col_stride;
+#pragma unroll
+            for (int i = 0; i < 8; i++) nxt[i] = q[(size_t)i * col_stride];
+        }
+        p2::permute(s);
+    }
+    if (rem) {
+        const uint64_t* q = p + (size_t)full * 8 * col_stride;
+#pragma unroll
+        for (int i = 0; i < 8; i++) s[i] = (uint32_t)i < rem ? q[(size_t)i * col_stride] : 0;
+        p2::permute(s);
+    }
+    uint64_t* o = out + 4 * L;
+#pragma unroll
+    for (int i = 0; i < 4; i++) o[i] = gl::canon(s[i]);
+}
+
+__device__ __forceinline__ void node_hash(const uint64_t* l, const uint64_t* r, uint64_t* o) {
+    uint64_t s[12];
+#pragma unroll
+    for (int i = 0; i < 4; i++) { s[i] = l[i]; s[4 + i] = r[i]; s[8 + i] = 0; }
+    p2::permute(s);
+#pragma unroll
+    for (int i = 0; i < 4; i++) o[i] = gl::canon(s[i]);
+}
+
+__global__ __launch_bounds__(256) void node_level_kernel(const uint64_t* __restrict__ prev,
+                                                         uint64_t* __restrict__ next, size_t m) {
+    const size_t i = blockIdx.x * (size_t)256 + threadIdx.x;
+    if (i >= m) return;
+    uint64_t lr[8];
+#pragma unroll
+    for (int k = 0; k < 8; k++) lr[k] = prev[8 * i + k];
+    node_hash(lr, lr + 4, next + 4 * i);
+}
+
+// Remaining levels from `len` digests (len <= 4096) down to cap_size, one workgroup.
+__global__ __launch_bounds__(256) void node_tail_kernel(const uint64_t* __restrict__ prev, uint64_t* next,
+                                                        uint32_t len, uint32_t cap_size) {
+    __shared__ uint64_t buf[2][2048 * 4];
+    int cur = 0;
+    uint64_t* outp = next;
+    // first level reads from global
+    uint32_t m = len / 2;
+    for (uint32_t i = threadIdx.x; i < m; i += 256) {
+        uint64_t lr[8];
+        for (int k = 0; k < 8; k++) lr[k] = prev[8 * (size_t)i + k];
+        uint64_t o[4];
+        node_hash(lr, lr + 4, o);
+        for (int k = 0; k < 4; k++) { buf[cur][4 * i + k] = o[k]; outp[4 * (size_t)i + k] = o[k]; }
+    }
+    outp += 4 * (size_t)m;
+    __syncthreads();
+    while (m > cap_size) {
+        uint32_t m2 = m / 2;
+        for (uint32_t i = threadIdx.x; i < m2; i += 256) {
+            uint64_t o[4];
+            node_hash(&buf[cur][8 * i], &buf[cur][8 * i + 4], o);
+            for (int k = 0; k < 4; k++) { buf[cur ^ 1][4 * i + k] = o[k]; outp[4 * (size_t)i + k] = o[k]; }
+        }
+        outp += 4 * (size_t)m2;
+        cur ^= 1;
+        m = m2;
+        __syncthreads();
+    }
+}
+
+__global__ __launch_bounds__(256) void permute_kernel(uint64_t* states, size_t count) {
+    const size_t i = blockIdx.x * (size_t)256 + threadIdx.x;
+    if (i >= count) return;
+    uint64_t s[12];
+#pragma unroll
+    for (int k = 0; k < 12; k++) s[k] = states[12 * i + k];
+    p2::permute(s);
+#pragma unroll
+    for (int k = 0; k < 12; k++) states[12 * i + k] = gl::canon(s[k]);
+}
+
+hipError_t launch_leaves(const uint64_t* src, size_t col_stride, uint32_t n_cols, size_t n_leaves, uint64_t* out,
+                         hipStream_t st) {
+    if (n_leaves == 0) return hipSuccess;
+    size_t blocks = (n_leaves + LEAF_THREADS - 1) / LEAF_THREADS;
+    hipLaunchKernelGGL(leaf_hash_kernel, dim3((unsigned)blocks), dim3(LEAF_THREADS), 0, st, src, col_stride,
+                       n_cols, n_leaves, out);
+    return hipGetLastError();
+}
+
+hipError_t launch_nodes(const uint64_t* leaves, size_t n_leaves, uint32_t cap_size, uint64_t* nodes,
+                        hipStream_t st) {
+    const uint64_t* prev = leaves;
+    uint64_t* out = nodes;
+    size_t len = n_leaves;
+    while (len > cap_size && len > 4096) {
+        size_t m = len / 2;
+        hipLaunchKernelGGL(node_level_kernel, dim3((unsigned)((m + 255) / 256)), dim3(256), 0, st, prev, out, m);
+        prev = out;
+        out += 4 * m;
+        len = m;
+    }
+    if (len > cap_size) {
+        hipLaunchKernelGGL(node_tail_kernel, dim3(1), dim3(256), 0, st, prev, out, (uint32_t)len, cap_size);
+    }
+    return hipGetLastError();
+}
+
+hipError_t launch_permute(uint64_t* states, size_t count, hipStream_t st) {
+    if (count == 0) return hipSuccess;
+    hipLaunchKernelGGL(permute_kernel, dim3((unsigned)((count + 255) / 256)), dim3(256), 0, st, states, count);
+    return hipGetLastError();
+}
+
+}  // namespace bj

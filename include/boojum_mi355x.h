@@ -1,0 +1,159 @@
+/*
+ * boojum_mi355x.h -- C ABI of the MI355X-native witness-commitment hot path
+ * (coset LDE over Goldilocks + Poseidon2 Merkle tree with cap).
+ *
+ * Library: era-boojum_amd/boojum_amd/libboojum_mi355x.so (hipcc, gfx950).
+ * Plain C types only: pointers, sizes, u64 field elements.  All field elements
+ * crossing this boundary are u64; outputs are canonical (< p = 2^64 - 2^32 + 1),
+ * inputs may be any u64 representative (as the reference's GoldilocksField,
+ * field/goldilocks/mod.rs:92-94).
+ *
+ * Return value: 0 on success, a negative errno-style code on failure
+ * (BJ_EINVAL for violated preconditions -- the reference asserts/panics on these,
+ * fft/mod.rs:399-402, utils.rs:284-287, merkle_tree.rs:83-96 -- BJ_EHIP for a HIP
+ * runtime error).  bj_last_error() gives a message for the calling thread.
+ * A Rust/ctypes shim maps non-zero to panic!/raise, keeping reference semantics.
+ *
+ * Two families:
+ *   *_d   device-resident batched entry points.  Pointers are device (HBM)
+ *         pointers; `stream` is a hipStream_t (NULL = default stream).  Calls are
+ *         asynchronous on the stream and never synchronise the device.  These are
+ *         what a batched GPU prover calls once per commitment.
+ *   *_h   host-pointer entry points with exactly the reference seam's per-call
+ *         semantics (in place, synchronous), for drop-in replacement of the
+ *         reference functions named in each comment.
+ *
+ * Thread safety: all entry points are re-entrant (the reference calls its FFT seam
+ * concurrently from rayon workers, cs/implementations/utils.rs:295-304,363-379).
+ * The only global state is a per-device cache of twiddle tables, filled under a
+ * lock on first use of a size (bj_prepare fills it ahead of time).
+ */
+#ifndef BOOJUM_MI355X_H
+#define BOOJUM_MI355X_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define BJ_OK 0
+#define BJ_EINVAL (-22)
+#define BJ_ENOMEM (-12)
+#define BJ_EHIP (-5)
+
+/* Message for the last failure on the calling thread ("" if none). */
+const char* bj_last_error(void);
+/* ABI version (major << 16 | minor). */
+uint32_t bj_abi_version(void);
+
+/* Fill the device twiddle cache for FFT size 2^log_n (forward + inverse tables) on the
+ * current device, synchronously.  Twiddle precompute is outside the timed region in
+ * the reference's own accounting (prover.rs:313-353 precomputes before "LDE taken"). */
+int bj_prepare(uint32_t log_n);
+
+/* ---------------------------------------------------------------- FFT seam */
+
+/* precompute_twiddles_for_fft::<INVERSED> (cs/implementations/utils.rs:88-125,
+ * wrapper fft/mod.rs:625-641): omega_n^i (or omega_n^-i), i < n/2, bit-reversed order.
+ * out_d: n/2 u64 (device). */
+int bj_precompute_twiddles_d(uint32_t log_n, int inverse, uint64_t* out_d, void* stream);
+int bj_precompute_twiddles_h(uint32_t log_n, int inverse, uint64_t* out_h);
+
+/* distribute_powers (fft/mod.rs:308-317): col[j] *= element^j, for n_cols columns of
+ * 2^log_n elements, column c at cols + c * col_stride. */
+int bj_distribute_powers_d(uint64_t* cols, uint32_t n_cols, size_t col_stride, uint32_t log_n,
+                           uint64_t element, void* stream);
+int bj_distribute_powers_h(uint64_t* col, size_t len, uint64_t element);
+
+/* fft_natural_to_bitreversed (fft/mod.rs:398-411; PrimeFieldLikeVectorized seam
+ * field/traits/field_like.rs:111-162): distribute_powers(coset) if coset != 1, then the
+ * radix-2 natural->bit-reversed transform (fft/mod.rs:659-734).  In place.
+ * twiddles may be NULL (the device cache is used); if given it must be the
+ * bj_precompute_twiddles output for this size (it is used as is). */
+int bj_fft_natural_to_bitreversed_d(uint64_t* cols, uint32_t n_cols, size_t col_stride, uint32_t log_n,
+                                    uint64_t coset, const uint64_t* twiddles_d, void* stream);
+int bj_fft_natural_to_bitreversed_h(uint64_t* col, size_t len, uint64_t coset);
+
+/* ifft_natural_to_natural (fft/mod.rs:464-491): inverse transform, bit-reverse, times
+ * coset^-j if coset != 1, times n^-1.  In place. */
+int bj_ifft_natural_to_natural_d(uint64_t* cols, uint32_t n_cols, size_t col_stride, uint32_t log_n,
+                                 uint64_t coset, const uint64_t* inv_twiddles_d, void* stream);
+int bj_ifft_natural_to_natural_h(uint64_t* col, size_t len, uint64_t coset);
+
+/* ------------------------------------------------------------------- LDE */
+
+/* transform_raw_storages_to_lde (cs/implementations/utils.rs:270-309 + :311-403, as
+ * driven by WitnessStorage::from_base_trace*, witness_storage.rs:18-116):
+ *   monomials[c] = ifft_natural_to_natural(trace[c])
+ *   lde[c][i]    = fft_natural_to_bitreversed(monomials[c], 7 * w_{nD}^{bitrev(i)})
+ * trace:     n_cols columns of n = 2^log_n at trace + c * trace_stride (read only)
+ * monomials: n_cols x n scratch/output, column c at monomials + c * n
+ * lde:       n_cols x D x n, element (c, i, r) at lde + (c * D + i) * n + r
+ *            (the reference's per-column Vec<coset> of ArcGenericLdeStorage)
+ * D = 2^log_lde. */
+int bj_lde_d(const uint64_t* trace, uint32_t n_cols, size_t trace_stride, uint32_t log_n,
+             uint32_t log_lde, uint64_t* monomials, uint64_t* lde, void* stream);
+
+/* Coset LDE of already-monomial columns (transform_monomials_to_lde, utils.rs:311-403;
+ * also the quotient commit path prover.rs:1471-1482).  monomials read only. */
+int bj_monomials_to_lde_d(const uint64_t* monomials, uint32_t n_cols, size_t mono_stride, uint32_t log_n,
+                          uint32_t log_lde, uint64_t* lde, void* stream);
+
+/* ---------------------------------------------------------- Poseidon2 / Merkle */
+
+/* poseidon2_permutation (implementations/poseidon2/state_generic_impl.rs:221-249) on
+ * `count` independent 12-element states, in place. */
+int bj_poseidon2_permute_d(uint64_t* states, size_t count, void* stream);
+int bj_poseidon2_permute_h(uint64_t* state12);
+
+/* TreeHasher::hash_into_leaf for GoldilocksPoseidon2Sponge<AbsorptionModeOverwrite>
+ * (cs/oracle/mod.rs:141-151, algebraic_props/sponge.rs:224-323) of n_elems elements. */
+int bj_hash_into_leaf_h(const uint64_t* elems, size_t n_elems, uint64_t* out4);
+/* TreeHasher::hash_into_node (cs/oracle/mod.rs:162-168). */
+int bj_hash_into_node_h(const uint64_t* left4, const uint64_t* right4, uint64_t* out4);
+
+/* Leaf hashing of MerkleTreeWithCap::construct (cs/oracle/merkle_tree.rs:78-172):
+ * leaf L (flat index coset * n + row) = hash_into_leaf(src[0][L], ..., src[n_cols-1][L]),
+ * column c's leaf-domain values at src + c * col_stride.  leaves: n_leaves x 4. */
+int bj_merkle_leaves_d(const uint64_t* src, uint32_t n_cols, size_t col_stride, size_t n_leaves,
+                       uint64_t* leaves, void* stream);
+
+/* continue_from_leaf_hashes (merkle_tree.rs:388-449): node levels from n_leaves leaves
+ * up to cap_size nodes.  nodes: (n_leaves - cap_size) x 4, the levels concatenated from
+ * the leaves upward (node_hashes_enumerated_from_leafs); the cap is the last cap_size
+ * digests (get_cap, merkle_tree.rs:451-460, canonical).  Requires n_leaves > cap_size,
+ * both powers of two. */
+int bj_merkle_nodes_d(const uint64_t* leaves, size_t n_leaves, uint32_t cap_size, uint64_t* nodes,
+                      void* stream);
+
+/* ------------------------------------------------------- whole commitment */
+
+/* Witness commitment, the batched hot path (prover.rs:313-353 with all D cosets
+ * committed, fri_lde_factor == lde degree): LDE of every column, Poseidon2 leaves over
+ * the n*D rows, node levels to the cap.  All pointers device; cap additionally copied
+ * to cap_h (host, cap_size x 4) if non-NULL (this synchronises the stream). */
+int bj_lde_commit_d(const uint64_t* trace, uint32_t n_cols, size_t trace_stride, uint32_t log_n,
+                    uint32_t log_lde, uint32_t cap_size, uint64_t* monomials, uint64_t* lde,
+                    uint64_t* leaves, uint64_t* nodes, uint64_t* cap_h, void* stream);
+
+/* Host-buffer variant (drop-in for a Rust prover that owns host Vecs): copies the trace
+ * in, runs bj_lde_commit_d, copies every output back.  Any output pointer may be NULL
+ * to skip its copy.  PCIe-inclusive; never the headline number. */
+int bj_lde_commit_h(const uint64_t* trace_h, uint32_t n_cols, uint32_t log_n, uint32_t log_lde,
+                    uint32_t cap_size, uint64_t* lde_h, uint64_t* leaves_h, uint64_t* nodes_h,
+                    uint64_t* cap_h);
+
+/* ------------------------------------------------------------- utility */
+
+/* Bench/test input (not a reference entry point): column-major synthetic trace,
+ * x = splitmix64(seed + (first_col + c) * n + r) reduced once mod p. */
+int bj_fill_synthetic_d(uint64_t* dst, uint32_t n_cols, size_t col_stride, uint32_t log_n, uint64_t seed,
+                        uint64_t first_col, void* stream);
+
+#ifdef __cplusplus
+}
+#endif
+
+#endif /* BOOJUM_MI355X_H */

@@ -1,0 +1,267 @@
+"""ctypes wrapper over oracle/liboracle.so -- CPU ORACLE, TEST INFRASTRUCTURE ONLY.
+
+Only tests/, __graft_entry__.smoke() and bench.py's cpu_baseline leg may import this
+module.  The product (era-boojum_amd/boojum_amd) never imports it.
+
+All arrays are numpy uint64; all outputs are canonical Goldilocks values.
+See boojum_oracle.c for the reference file:line each function restates.
+"""
+import ctypes
+import os
+
+import numpy as np
+
+P = 0xFFFFFFFF00000001
+_HERE = os.path.dirname(os.path.abspath(__file__))
+_LIB = None
+
+_u64p = ctypes.POINTER(ctypes.c_uint64)
+
+
+def lib():
+    global _LIB
+    if _LIB is None:
+        path = os.path.join(_HERE, "liboracle.so")
+        if not os.path.exists(path):
+            raise RuntimeError("oracle/liboracle.so missing: run `make -C oracle` "
+                               "(or __graft_entry__.build())")
+        L = ctypes.CDLL(path)
+        u64, sz, u32, i = ctypes.c_uint64, ctypes.c_size_t, ctypes.c_uint32, ctypes.c_int
+        for name in ("bjo_gl_add", "bjo_gl_sub", "bjo_gl_mul", "bjo_gl_pow"):
+            getattr(L, name).restype = u64
+            getattr(L, name).argtypes = [u64, u64]
+        L.bjo_gl_inv.restype = u64
+        L.bjo_gl_inv.argtypes = [u64]
+        L.bjo_domain_generator.restype = u64
+        L.bjo_domain_generator.argtypes = [u32]
+        L.bjo_bitreverse_inplace.argtypes = [_u64p, sz]
+        L.bjo_precompute_twiddles.argtypes = [u32, i, _u64p]
+        L.bjo_distribute_powers.argtypes = [_u64p, sz, u64]
+        L.bjo_fft_natural_to_bitreversed.argtypes = [_u64p, sz, u64, _u64p]
+        L.bjo_ifft_natural_to_natural.argtypes = [_u64p, sz, u64, _u64p]
+        L.bjo_lde_cosets.argtypes = [u32, u32, _u64p]
+        L.bjo_lde.argtypes = [_u64p, u32, u32, u32, _u64p, i]
+        L.bjo_poseidon2_permute_canonical.argtypes = [_u64p]
+        L.bjo_hash_into_leaf.argtypes = [_u64p, sz, _u64p]
+        L.bjo_hash_into_node.argtypes = [_u64p, _u64p, _u64p]
+        L.bjo_merkle_construct.restype = i
+        L.bjo_merkle_construct.argtypes = [_u64p, sz, u32, sz, u32, _u64p, _u64p, i]
+        L.bjo_merkle_get_proof.argtypes = [_u64p, _u64p, sz, i, sz, _u64p, _u64p]
+        L.bjo_verify_proof_over_cap.restype = i
+        L.bjo_verify_proof_over_cap.argtypes = [_u64p, i, _u64p, _u64p, sz]
+        L.bjo_lde_commit.restype = i
+        L.bjo_lde_commit.argtypes = [_u64p, u32, u32, u32, u32, _u64p, _u64p, _u64p, _u64p, i]
+        L.bjo_find_query_index.restype = ctypes.c_long
+        L.bjo_find_query_index.argtypes = [_u64p, _u64p, i, _u64p, sz]
+        _LIB = L
+    return _LIB
+
+
+def _p(a):
+    assert a.dtype == np.uint64 and a.flags["C_CONTIGUOUS"], (a.dtype, a.flags)
+    return a.ctypes.data_as(_u64p)
+
+
+def _u64(x):
+    return np.ascontiguousarray(np.asarray(x, dtype=np.uint64))
+
+
+def gl_mul(a, b):
+    return lib().bjo_gl_mul(a, b)
+
+
+def gl_add(a, b):
+    return lib().bjo_gl_add(a, b)
+
+
+def gl_sub(a, b):
+    return lib().bjo_gl_sub(a, b)
+
+
+def gl_pow(a, e):
+    return lib().bjo_gl_pow(a, e)
+
+
+def gl_inv(a):
+    return lib().bjo_gl_inv(a)
+
+
+def domain_generator(log_n):
+    return lib().bjo_domain_generator(log_n)
+
+
+def precompute_twiddles(log_n, inverse=False):
+    out = np.zeros(max(1, (1 << log_n) // 2), dtype=np.uint64)
+    lib().bjo_precompute_twiddles(log_n, 1 if inverse else 0, _p(out))
+    return out[: (1 << log_n) // 2]
+
+
+def bitreverse(a):
+    a = _u64(a).copy()
+    lib().bjo_bitreverse_inplace(_p(a), a.size)
+    return a
+
+
+def distribute_powers(a, element):
+    a = _u64(a).copy()
+    lib().bjo_distribute_powers(_p(a), a.size, element)
+    return a
+
+
+def fft_natural_to_bitreversed(a, coset=1):
+    a = _u64(a).copy()
+    log_n = a.size.bit_length() - 1
+    tw = precompute_twiddles(log_n, False) if a.size > 1 else np.zeros(1, np.uint64)
+    tw = np.ascontiguousarray(tw if tw.size else np.zeros(1, np.uint64))
+    lib().bjo_fft_natural_to_bitreversed(_p(a), a.size, coset, _p(tw))
+    return a
+
+
+def ifft_natural_to_natural(a, coset=1):
+    a = _u64(a).copy()
+    log_n = a.size.bit_length() - 1
+    tw = precompute_twiddles(log_n, True) if a.size > 1 else np.zeros(1, np.uint64)
+    tw = np.ascontiguousarray(tw if tw.size else np.zeros(1, np.uint64))
+    lib().bjo_ifft_natural_to_natural(_p(a), a.size, coset, _p(tw))
+    return a
+
+
+def lde_cosets(log_n, log_d):
+    out = np.zeros(1 << log_d, dtype=np.uint64)
+    lib().bjo_lde_cosets(log_n, log_d, _p(out))
+    return out
+
+
+def lde(trace, log_d, threads=1):
+    """trace: (C, n) uint64 -> (monomials (C, n), lde (C, D, n))"""
+    tr = _u64(trace).copy()
+    c, n = tr.shape
+    log_n = n.bit_length() - 1
+    out = np.zeros((c, 1 << log_d, n), dtype=np.uint64)
+    lib().bjo_lde(_p(tr), c, log_n, log_d, _p(out), threads)
+    return tr, out
+
+
+def poseidon2_permutation(state):
+    s = _u64(state).copy()
+    assert s.size == 12
+    lib().bjo_poseidon2_permute_canonical(_p(s))
+    return s
+
+
+def hash_into_leaf(elems):
+    e = _u64(elems)
+    if e.size == 0:
+        e = np.zeros(1, np.uint64)
+        n = 0
+    else:
+        n = e.size
+    out = np.zeros(4, dtype=np.uint64)
+    lib().bjo_hash_into_leaf(_p(e), n, _p(out))
+    return out
+
+
+def hash_into_node(left, right):
+    l, r = _u64(left), _u64(right)
+    out = np.zeros(4, dtype=np.uint64)
+    lib().bjo_hash_into_node(_p(l), _p(r), _p(out))
+    return out
+
+
+def num_node_levels(n_leaves, cap_size):
+    return (n_leaves.bit_length() - 1) - (cap_size.bit_length() - 1)
+
+
+def merkle_construct(lde_flat, cap_size, threads=1):
+    """lde_flat: (C, n_leaves) uint64 (column c's values over the flat leaf index).
+    Returns (leaves (n_leaves, 4), nodes (sum of levels, 4), levels, cap (cap_size, 4))."""
+    src = _u64(lde_flat)
+    c, nl = src.shape
+    levels = num_node_levels(nl, cap_size)
+    leaves = np.zeros((nl, 4), dtype=np.uint64)
+    n_nodes = nl - cap_size if levels > 0 else 0
+    nodes = np.zeros((max(n_nodes, 1), 4), dtype=np.uint64)
+    got = lib().bjo_merkle_construct(_p(src), nl, c, nl, cap_size, _p(leaves), _p(nodes), threads)
+    assert got == levels
+    cap = nodes[n_nodes - cap_size: n_nodes].copy() if levels > 0 else leaves.copy()
+    return leaves, nodes[:n_nodes], levels, cap
+
+
+def merkle_get_proof(leaves, nodes, levels, idx):
+    nl = leaves.shape[0]
+    leaf = np.zeros(4, dtype=np.uint64)
+    path = np.zeros((max(levels, 1), 4), dtype=np.uint64)
+    nd = nodes if nodes.size else np.zeros((1, 4), np.uint64)
+    lib().bjo_merkle_get_proof(_p(_u64(leaves)), _p(_u64(nd)), nl, levels, idx, _p(leaf), _p(path))
+    return leaf, path[:levels]
+
+
+def verify_proof_over_cap(path, cap, leaf, idx):
+    path = _u64(path).reshape(-1, 4)
+    pp = path if path.size else np.zeros((1, 4), np.uint64)
+    return bool(lib().bjo_verify_proof_over_cap(_p(pp), path.shape[0], _p(_u64(cap)), _p(_u64(leaf)), idx))
+
+
+def lde_commit(trace, log_d, cap_size, threads=1):
+    """Full witness commit (oracle).  Returns dict with monomials, lde (C, D, n),
+    leaves, nodes, cap."""
+    tr = _u64(trace).copy()
+    c, n = tr.shape
+    log_n = n.bit_length() - 1
+    nl = n << log_d
+    lde_out = np.zeros((c, 1 << log_d, n), dtype=np.uint64)
+    leaves = np.zeros((nl, 4), dtype=np.uint64)
+    n_nodes = nl - cap_size
+    nodes = np.zeros((max(n_nodes, 1), 4), dtype=np.uint64)
+    cap = np.zeros((cap_size, 4), dtype=np.uint64)
+    lib().bjo_lde_commit(_p(tr), c, log_n, log_d, cap_size, _p(lde_out), _p(leaves), _p(nodes), _p(cap), threads)
+    return {"monomials": tr, "lde": lde_out, "leaves": leaves, "nodes": nodes[:n_nodes], "cap": cap}
+
+
+def find_query_index(leaf, path, cap):
+    path = _u64(path).reshape(-1, 4)
+    cap = _u64(cap).reshape(-1, 4)
+    return lib().bjo_find_query_index(_p(_u64(leaf)), _p(path), path.shape[0], _p(cap), cap.shape[0])
+
+
+# ----------------------------------------------------------- pure-python helpers
+
+def splitmix64(x):
+    """splitmix64 finaliser on a uint64 numpy array (synthetic inputs)."""
+    x = np.asarray(x, dtype=np.uint64)
+    with np.errstate(over="ignore"):
+        z = x + np.uint64(0x9E3779B97F4A7C15)
+        z = (z ^ (z >> np.uint64(30))) * np.uint64(0xBF58476D1CE4E5B9)
+        z = (z ^ (z >> np.uint64(27))) * np.uint64(0x94D049BB133111EB)
+        z = z ^ (z >> np.uint64(31))
+    return z
+
+
+def synthetic_trace(n_cols, log_n, seed=42, col_offset=0):
+    """Column-major canonical trace: x = splitmix64(seed + c*n + r), reduced once."""
+    n = 1 << log_n
+    idx = (np.arange(col_offset, col_offset + n_cols, dtype=np.uint64)[:, None] * np.uint64(n)
+           + np.arange(n, dtype=np.uint64)[None, :] + np.uint64(seed))
+    x = splitmix64(idx)
+    return np.where(x >= np.uint64(P), x - np.uint64(P), x)
+
+
+def naive_coset_lde_column(col, log_d):
+    """Closed form: LDE[L] = p(7 * w_{nD}^{bitrev_{log nD}(L)}), p the
+    interpolant of `col` over <w_n>.  Pure python, tiny n only (reference test
+    methodology fft/mod.rs:1591-1634)."""
+    n = len(col)
+    log_n = n.bit_length() - 1
+    mono = [int(v) for v in ifft_natural_to_natural(col)]
+    nd = n << log_d
+    bits = log_n + log_d
+    g = domain_generator(bits)
+    out = []
+    for L in range(nd):
+        r = int(format(L, "0%db" % bits)[::-1], 2) if bits else 0
+        x = (7 * pow(g, r, P)) % P
+        acc = 0
+        for c in reversed(mono):
+            acc = (acc * x + c) % P
+        out.append(acc)
+    return out

@@ -1,0 +1,236 @@
+"""GPU parity: the HIP path (through the C ABI) against the CPU oracle, bit-exact.
+
+Sizes are ones the oracle finishes in seconds.  Full-size (BASELINE configs) checks are
+in test_gpu_fullsize.py.  Edge cases follow what the reference's tests and asserts
+cover: ragged column counts (leaf lengths not multiples of the rate 8), n = 1 and 2,
+non-canonical inputs, all-zero / all-(p-1) / impulse columns, every LDE degree used.
+"""
+import numpy as np
+import pytest
+
+import oracle as O
+
+pytestmark = pytest.mark.gpu
+
+P = O.P
+
+
+@pytest.fixture(scope="module")
+def bj():
+    import torch
+    assert torch.cuda.is_available(), "gpu tests need a GPU"
+    import boojum_amd
+    from boojum_amd import commit, fft, field, lde, merkle
+    boojum_amd.load()
+    return type("BJ", (), dict(torch=torch, fft=fft, field=field, lde=lde, merkle=merkle, commit=commit))
+
+
+def rand(shape, seed):
+    return np.random.default_rng(seed).integers(0, P, size=shape, dtype=np.uint64)
+
+
+def eq(a, b):
+    a = np.asarray(a, dtype=np.uint64)
+    b = np.asarray(b, dtype=np.uint64)
+    assert a.shape == b.shape, (a.shape, b.shape)
+    bad = np.argwhere(a != b)
+    assert bad.size == 0, "first mismatches at %s" % bad[:5].tolist()
+
+
+# -------------------------------------------------------------- Poseidon2
+
+def test_permutation_kats(bj):
+    s = bj.merkle.Poseidon2Sponge.poseidon2_permutation(np.arange(12))
+    assert [int(x) for x in s[:4]] == [0x5d82c16b87f07f98, 0x3655af22bb2f037d, 0x82c1535dfb4bdf90,
+                                       0x4d318cfdafd2378e]
+
+
+def test_permutation_batch_random_and_edge(bj):
+    st = rand((4096, 12), 1)
+    st[0] = 0
+    st[1] = P - 1
+    st[2] = np.uint64(2**64 - 1)  # non-canonical representative
+    st[3, :] = np.arange(12, dtype=np.uint64) + np.uint64(P)
+    t = bj.field.to_device(st)
+    from boojum_amd._lib import call
+    call("bj_poseidon2_permute_d", t.data_ptr(), st.shape[0], bj.field.stream_of(t))
+    got = bj.field.to_host(t)
+    want = np.stack([O.poseidon2_permutation(np.array([int(x) % P for x in row], dtype=np.uint64)) for row in st])
+    eq(got, want)
+
+
+@pytest.mark.parametrize("n", [0, 1, 3, 7, 8, 9, 16, 58, 156, 167, 256, 257])
+def test_hash_into_leaf(bj, n):
+    x = rand(n, n + 100)
+    eq(bj.merkle.Poseidon2Sponge.hash_into_leaf(x), O.hash_into_leaf(x))
+
+
+def test_hash_into_node(bj):
+    l, r = rand(4, 1), rand(4, 2)
+    eq(bj.merkle.Poseidon2Sponge.hash_into_node(l, r), O.hash_into_node(l, r))
+
+
+def test_proof_json_paths_verify_on_gpu(bj):
+    import json
+    import os
+    fx = json.load(open(os.path.join(os.path.dirname(__file__), "golden", "proof_queries.json")))
+    T = bj.merkle.MerkleTreeWithCap
+    for q in fx["queries"][:3]:
+        for name in ("witness", "stage_2", "quotient", "setup"):
+            e = q[name]
+            leaf = bj.merkle.Poseidon2Sponge.hash_into_leaf(e["leaf_elements"])
+            assert T.verify_proof_over_cap(e["proof"], fx["caps"][name], leaf, q["index"])
+
+
+# -------------------------------------------------------------------- FFT
+
+@pytest.mark.parametrize("log_n", [1, 2, 3, 5, 8, 12, 13, 16, 17])
+def test_twiddles(bj, log_n):
+    for inv in (False, True):
+        t = bj.fft.precompute_twiddles_for_fft(1 << log_n, inverse=inv)
+        eq(bj.field.to_host(t), O.precompute_twiddles(log_n, inv))
+
+
+@pytest.mark.parametrize("log_n", [0, 1, 2, 4, 7, 11, 12, 13, 15, 20, 21])
+def test_fft_natural_to_bitreversed_batch(bj, log_n):
+    c = 3 if log_n < 20 else 1
+    x = rand((c, 1 << log_n), log_n)
+    x[0, 0] = np.uint64(2**64 - 1)  # non-canonical input
+    for coset in (1, 7, 0x1234567):
+        t = bj.field.to_device(x)
+        bj.fft.fft_natural_to_bitreversed(t, coset)
+        want = np.stack([O.fft_natural_to_bitreversed(x[i], coset) for i in range(c)])
+        eq(bj.field.to_host(t), want)
+
+
+@pytest.mark.parametrize("log_n", [0, 1, 2, 3, 6, 10, 12, 13, 14, 19])
+def test_ifft_natural_to_natural_batch(bj, log_n):
+    x = rand((2, 1 << log_n), 50 + log_n)
+    for coset in (1, 7):
+        t = bj.field.to_device(x)
+        bj.fft.ifft_natural_to_natural(t, coset)
+        want = np.stack([O.ifft_natural_to_natural(x[i], coset) for i in range(2)])
+        eq(bj.field.to_host(t), want)
+
+
+def test_distribute_powers(bj):
+    x = rand((2, 1 << 14), 5)
+    t = bj.field.to_device(x)
+    bj.fft.distribute_powers(t, 0xdeadbeef)
+    eq(bj.field.to_host(t), np.stack([O.distribute_powers(x[i], 0xdeadbeef) for i in range(2)]))
+
+
+def test_host_seam_in_place(bj):
+    x = rand(1 << 10, 9)
+    y = x.copy()
+    bj.fft.fft_natural_to_bitreversed_host(y, 7)
+    eq(y, O.fft_natural_to_bitreversed(x, 7))
+    z = x.copy()
+    bj.fft.ifft_natural_to_natural_host(z, 1)
+    eq(z, O.ifft_natural_to_natural(x, 1))
+    w = x.copy()
+    bj.fft.distribute_powers_host(w, 11)
+    eq(w, O.distribute_powers(x, 11))
+    eq(bj.fft.precompute_twiddles_for_fft_host(1 << 10, True), O.precompute_twiddles(10, True))
+
+
+# -------------------------------------------------------------------- LDE
+
+@pytest.mark.parametrize("c,log_n,log_d", [(1, 0, 1), (2, 1, 1), (3, 3, 2), (5, 6, 3), (4, 12, 1), (3, 13, 2),
+                                           (2, 16, 3), (1, 17, 1)])
+def test_lde_batch(bj, c, log_n, log_d):
+    x = rand((c, 1 << log_n), c * 100 + log_n)
+    t = bj.field.to_device(x)
+    mono, l = bj.lde.transform_raw_storages_to_lde(t, 1 << log_d)
+    m_ref, l_ref = O.lde(x, log_d, threads=4)
+    eq(bj.field.to_host(mono), m_ref)
+    eq(bj.field.to_host(l), l_ref)
+
+
+def test_lde_edge_columns(bj):
+    n = 1 << 10
+    x = np.zeros((4, n), dtype=np.uint64)
+    x[1, :] = P - 1
+    x[2, 5] = 1
+    x[3, :] = np.uint64(2**64 - 1)  # all non-canonical (== 2^32 - 2 mod p)
+    t = bj.field.to_device(x)
+    mono, l = bj.lde.transform_raw_storages_to_lde(t, 4)
+    m_ref, l_ref = O.lde(x, 2)
+    eq(bj.field.to_host(mono), m_ref)
+    eq(bj.field.to_host(l), l_ref)
+    assert not bj.field.to_host(l)[0].any()
+
+
+def test_lde_with_strided_trace(bj):
+    # trace columns inside a wider buffer (col_stride > n)
+    x = rand((3, 1 << 11), 77)
+    big = np.zeros((3, 3 << 11), dtype=np.uint64)
+    big[:, : 1 << 11] = x
+    t = bj.field.to_device(big)[:, : 1 << 11]
+    mono, l = bj.lde.transform_raw_storages_to_lde(t, 2)
+    m_ref, l_ref = O.lde(x, 1)
+    eq(bj.field.to_host(l), l_ref)
+
+
+# ------------------------------------------------------------------ Merkle
+
+@pytest.mark.parametrize("c,nl,cap", [(1, 2, 1), (5, 64, 4), (8, 1024, 16), (13, 4096, 1), (33, 1 << 13, 16),
+                                      (16, 1 << 14, 2048)])
+def test_merkle_tree(bj, c, nl, cap):
+    src = rand((c, nl), c + nl)
+    t = bj.field.to_device(src)
+    tree = bj.merkle.MerkleTreeWithCap.construct(t, cap)
+    leaves, nodes, levels, capr = O.merkle_construct(src, cap, threads=4)
+    eq(bj.field.to_host(tree.leaf_hashes), leaves)
+    eq(bj.field.to_host(tree.nodes), nodes)
+    eq(tree.get_cap(), capr)
+    for idx in (0, nl - 1, nl // 3):
+        leaf, path = tree.get_proof(idx)
+        assert bj.merkle.MerkleTreeWithCap.verify_proof_over_cap(path, tree.get_cap(), leaf, idx)
+
+
+# --------------------------------------------------------------- commit
+
+@pytest.mark.parametrize("c,log_n,log_d,cap", [(32, 16, 1, 16), (7, 10, 2, 8), (9, 9, 3, 16), (1, 4, 1, 2)])
+def test_witness_commit_matches_oracle(bj, c, log_n, log_d, cap):
+    """Config 1 (2^16 x 32, LDE 2, cap 16) end to end, plus ragged shapes."""
+    tr_np = O.synthetic_trace(c, log_n)
+    tr = bj.commit.synthetic_trace(c, log_n)
+    eq(bj.field.to_host(tr), tr_np)
+    ws = bj.commit.witness_commit(tr, 1 << log_d, cap)
+    ref = O.lde_commit(tr_np, log_d, cap, threads=8)
+    eq(bj.field.to_host(ws.monomials), ref["monomials"])
+    eq(bj.field.to_host(ws.lde), ref["lde"])
+    eq(bj.field.to_host(ws.leaves), ref["leaves"])
+    eq(bj.field.to_host(ws.nodes), ref["nodes"])
+    eq(bj.field.to_host(ws.cap), ref["cap"])
+
+
+def test_commit_host_abi_matches(bj):
+    import ctypes
+    from boojum_amd._lib import call
+    c, log_n, log_d, cap = 5, 8, 2, 4
+    tr = O.synthetic_trace(c, log_n)
+    nl = 1 << (log_n + log_d)
+    lde = np.zeros((c, 1 << log_d, 1 << log_n), dtype=np.uint64)
+    leaves = np.zeros((nl, 4), dtype=np.uint64)
+    nodes = np.zeros((nl - cap, 4), dtype=np.uint64)
+    capo = np.zeros((cap, 4), dtype=np.uint64)
+    p = lambda a: a.ctypes.data_as(ctypes.POINTER(ctypes.c_uint64))  # noqa: E731
+    call("bj_lde_commit_h", p(np.ascontiguousarray(tr)), c, log_n, log_d, cap, p(lde), p(leaves), p(nodes), p(capo))
+    ref = O.lde_commit(tr, log_d, cap)
+    eq(lde, ref["lde"])
+    eq(leaves, ref["leaves"])
+    eq(nodes, ref["nodes"])
+    eq(capo, ref["cap"])
+
+
+def test_errors_are_loud(bj):
+    from boojum_amd import BoojumError
+    t = bj.torch.zeros((2, 24), dtype=bj.torch.int64, device="cuda")
+    with pytest.raises((BoojumError, ValueError)):
+        bj.fft.fft_natural_to_bitreversed(t, 1)
+    with pytest.raises((BoojumError, ValueError)):
+        bj.lde.transform_raw_storages_to_lde(bj.torch.zeros((2, 16), dtype=bj.torch.int64, device="cuda"), 1)
+    with pytest.raises((BoojumError, ValueError)):
+        bj.merkle.MerkleTreeWithCap.construct(bj.torch.zeros((2, 16), dtype=bj.torch.int64, device="cuda"), 16)
