@@ -25,6 +25,8 @@ hipError_t launch_permute(uint64_t* states, size_t count, hipStream_t st);
 hipError_t launch_synthetic(uint64_t* dst, size_t col_stride, uint32_t n_cols, uint32_t log_n, uint64_t seed,
                             uint64_t col0, hipStream_t st);
 
+hipError_t launch_gl_op(int op, const uint64_t* a, const uint64_t* b, uint64_t* out, size_t n, hipStream_t st);
+
 // power table sizes for a column of 2^log_n: lo 4096, hi max(1, n / 4096)
 inline size_t pw_hi_len(uint32_t log_n) { return log_n > 12 ? ((size_t)1 << (log_n - 12)) : 1; }
 

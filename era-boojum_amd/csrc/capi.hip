@@ -248,6 +248,12 @@ int bj_fill_synthetic_d(uint64_t* dst, uint32_t n_cols, size_t col_stride, uint3
     return BJ_OK;
 }
 
+int bj_gl_op_d(int op, const uint64_t* a, const uint64_t* b, uint64_t* out, size_t n, void* stream) {
+    if (op < 0 || op > 4) return fail(BJ_EINVAL, "op must be 0 mul, 1 add, 2 sub, 3 reduce, 4 canon");
+    HIP_TRY(bj::launch_gl_op(op, a, b, out, n, S(stream)), "gl_op");
+    return BJ_OK;
+}
+
 int bj_poseidon2_permute_d(uint64_t* states, size_t count, void* stream) {
     HIP_TRY(bj::launch_permute(states, count, S(stream)), "permute");
     return BJ_OK;

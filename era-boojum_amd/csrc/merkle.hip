@@ -19,15 +19,42 @@ namespace bj {
 
 constexpr int LEAF_THREADS = 256;
 
+// Store the first `n` state words canonicalised (to_reduced_u64, goldilocks/mod.rs:146-153).
+__device__ __forceinline__ void store_canon4(const p2::State& s, uint64_t* o) {
+    uint32_t z0[4], z1[4];
+    glasm::canon_x4(s.lo[0], s.hi[0], z0[0], z1[0], s.lo[1], s.hi[1], z0[1], z1[1],
+                    s.lo[2], s.hi[2], z0[2], z1[2], s.lo[3], s.hi[3], z0[3], z1[3]);
+#pragma unroll
+    for (int i = 0; i < 4; i++) o[i] = ((uint64_t)z1[i] << 32) | z0[i];
+}
+
+__device__ __forceinline__ void store_canon4_at(const p2::State& s, int q, uint64_t* o) {
+    const int b = 4 * q;
+    uint32_t z0[4], z1[4];
+    glasm::canon_x4(s.lo[b], s.hi[b], z0[0], z1[0], s.lo[b + 1], s.hi[b + 1], z0[1], z1[1],
+                    s.lo[b + 2], s.hi[b + 2], z0[2], z1[2], s.lo[b + 3], s.hi[b + 3], z0[3], z1[3]);
+#pragma unroll
+    for (int i = 0; i < 4; i++) o[i] = ((uint64_t)z1[i] << 32) | z0[i];
+}
+
+__device__ __forceinline__ void load8(p2::State& s, const uint64_t* q, size_t stride, uint32_t count) {
+#pragma unroll
+    for (int i = 0; i < 8; i++) {
+        uint64_t v = (uint32_t)i < count ? q[(size_t)i * stride] : 0;
+        s.lo[i] = (uint32_t)v;
+        s.hi[i] = (uint32_t)(v >> 32);
+    }
+}
+
 __global__ __launch_bounds__(LEAF_THREADS) void leaf_hash_kernel(const uint64_t* __restrict__ src,
                                                                  size_t col_stride, uint32_t n_cols,
                                                                  size_t n_leaves, uint64_t* __restrict__ out) {
     const size_t L = blockIdx.x * (size_t)LEAF_THREADS + threadIdx.x;
     if (L >= n_leaves) return;
     const uint64_t* p = src + L;
-    uint64_t s[12];
+    p2::State s;
 #pragma unroll
-    for (int i = 0; i < 12; i++) s[i] = 0;
+    for (int i = 0; i < 12; i++) s.lo[i] = s.hi[i] = 0;
     const uint32_t full = n_cols >> 3;
     const uint32_t rem = n_cols & 7;
     // software prefetch: the next group's 8 loads are issued before this group's permute
@@ -38,7 +65,10 @@ __global__ __launch_bounds__(LEAF_THREADS) void leaf_hash_kernel(const uint64_t*
     }
     for (uint32_t g = 0; g < full; g++) {
 #pragma unroll
-        for (int i = 0; i < 8; i++) s[i] = nxt[i];
+        for (int i = 0; i < 8; i++) {
+            s.lo[i] = (uint32_t)nxt[i];
+            s.hi[i] = (uint32_t)(nxt[i] >> 32);
+        }
         if (g + 1 < full) {
             const uint64_t* q = p + (size_t)(g + 1) * 8 * col_stride;
 #pragma unroll
@@ -47,23 +77,24 @@ __global__ __launch_bounds__(LEAF_THREADS) void leaf_hash_kernel(const uint64_t*
         p2::permute(s);
     }
     if (rem) {
-        const uint64_t* q = p + (size_t)full * 8 * col_stride;
-#pragma unroll
-        for (int i = 0; i < 8; i++) s[i] = (uint32_t)i < rem ? q[(size_t)i * col_stride] : 0;
+        load8(s, p + (size_t)full * 8 * col_stride, col_stride, rem);
         p2::permute(s);
     }
-    uint64_t* o = out + 4 * L;
-#pragma unroll
-    for (int i = 0; i < 4; i++) o[i] = gl::canon(s[i]);
+    store_canon4(s, out + 4 * L);
 }
 
 __device__ __forceinline__ void node_hash(const uint64_t* l, const uint64_t* r, uint64_t* o) {
-    uint64_t s[12];
+    p2::State s;
 #pragma unroll
-    for (int i = 0; i < 4; i++) { s[i] = l[i]; s[4 + i] = r[i]; s[8 + i] = 0; }
+    for (int i = 0; i < 4; i++) {
+        s.lo[i] = (uint32_t)l[i];
+        s.hi[i] = (uint32_t)(l[i] >> 32);
+        s.lo[4 + i] = (uint32_t)r[i];
+        s.hi[4 + i] = (uint32_t)(r[i] >> 32);
+        s.lo[8 + i] = s.hi[8 + i] = 0;
+    }
     p2::permute(s);
-#pragma unroll
-    for (int i = 0; i < 4; i++) o[i] = gl::canon(s[i]);
+    store_canon4(s, o);
 }
 
 __global__ __launch_bounds__(256) void node_level_kernel(const uint64_t* __restrict__ prev,
@@ -82,7 +113,6 @@ __global__ __launch_bounds__(256) void node_tail_kernel(const uint64_t* __restri
     __shared__ uint64_t buf[2][2048 * 4];
     int cur = 0;
     uint64_t* outp = next;
-    // first level reads from global
     uint32_t m = len / 2;
     for (uint32_t i = threadIdx.x; i < m; i += 256) {
         uint64_t lr[8];
@@ -110,12 +140,16 @@ __global__ __launch_bounds__(256) void node_tail_kernel(const uint64_t* __restri
 __global__ __launch_bounds__(256) void permute_kernel(uint64_t* states, size_t count) {
     const size_t i = blockIdx.x * (size_t)256 + threadIdx.x;
     if (i >= count) return;
-    uint64_t s[12];
+    p2::State s;
 #pragma unroll
-    for (int k = 0; k < 12; k++) s[k] = states[12 * i + k];
+    for (int k = 0; k < 12; k++) {
+        uint64_t v = states[12 * i + k];
+        s.lo[k] = (uint32_t)v;
+        s.hi[k] = (uint32_t)(v >> 32);
+    }
     p2::permute(s);
 #pragma unroll
-    for (int k = 0; k < 12; k++) states[12 * i + k] = gl::canon(s[k]);
+    for (int q = 0; q < 3; q++) store_canon4_at(s, q, states + 12 * i + 4 * q);
 }
 
 hipError_t launch_leaves(const uint64_t* src, size_t col_stride, uint32_t n_cols, size_t n_leaves, uint64_t* out,

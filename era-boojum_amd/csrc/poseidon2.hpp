@@ -9,122 +9,168 @@
 // (state_generic_impl.rs:71-84, 166-202).  Round constants: poseidon2_rc.inc (data
 // extracted by tools/gen_poseidon2_constants.py from poseidon_goldilocks_params.rs).
 //
-// The state lives in 24 VGPRs (one permutation per lane).  Linear layers are evaluated
-// lazily: 64-bit limbs plus a 32-bit overflow word, reduced once per output, which
-// yields the same field elements as the reference's per-add reduction (all results are
-// compared in canonical form).
+// gfx950 formulation (same field values; every result is compared canonically):
+// * state element = (lo, hi) 32-bit halves of a u64 representative, one permutation per lane;
+// * linear layers run on "limbs": L = sum c_j lo_j and H = sum c_j hi_j in 64-bit lanes,
+//   so a linear combination never carries (coefficients here stay < 2^16); the round
+//   constant is added into the limbs, and one 5-instruction reduction
+//   (glasm::reduce_xN) turns (L, H) back into a u64 per element;
+// * S-box multiplies are the interleaved inline-asm products of gl_asm.hpp.
 #pragma once
 #include "gl.hpp"
+#include "gl_asm.hpp"
 
 namespace p2 {
 
-__device__ __constant__ static const uint64_t RC[30][12] = {
+// Round constants split into 64-bit (value, 0) pairs so a scalar load yields an SGPR pair
+// that v_lshl_add_u64 adds to a limb directly.
+struct RcLimbs {
+    uint64_t lo[30][12];
+    uint64_t hi[30][12];
+};
+
+constexpr uint64_t RC_FLAT[30][12] = {
 #include "poseidon2_rc.inc"
 };
 
-// Wide (lazy) value: lo + hi * 2^64, hi small.
-struct W {
-    uint64_t lo;
-    uint32_t hi;
+constexpr RcLimbs make_rc_limbs() {
+    RcLimbs r{};
+    for (int i = 0; i < 30; i++)
+        for (int j = 0; j < 12; j++) {
+            r.lo[i][j] = RC_FLAT[i][j] & 0xFFFFFFFFull;
+            r.hi[i][j] = RC_FLAT[i][j] >> 32;
+        }
+    return r;
+}
+
+__device__ __constant__ static const RcLimbs RCL = make_rc_limbs();
+
+struct State {
+    uint32_t lo[12], hi[12];
 };
 
-__device__ __forceinline__ W w_of(uint64_t x) { return W{x, 0u}; }
-
-__device__ __forceinline__ W w_add(W a, W b) {
-    uint64_t lo = a.lo + b.lo;
-    uint32_t hi = a.hi + b.hi + (lo < a.lo ? 1u : 0u);
-    return W{lo, hi};
+// x^7 for 4 independent elements: x2 = x^2; x3 = x2*x, x4 = x2^2; x7 = x3*x4.
+__device__ __forceinline__ void sbox_x4(uint32_t* lo, uint32_t* hi) {
+    uint32_t a0, a1, b0, b1, c0, c1, d0, d1;  // x2 of the four
+    glasm::mul_x4(lo[0], hi[0], lo[0], hi[0], a0, a1, lo[1], hi[1], lo[1], hi[1], b0, b1,
+                  lo[2], hi[2], lo[2], hi[2], c0, c1, lo[3], hi[3], lo[3], hi[3], d0, d1);
+    uint32_t e0, e1, f0, f1, g0, g1, h0, h1;  // x3 of the four
+    glasm::mul_x4(a0, a1, lo[0], hi[0], e0, e1, b0, b1, lo[1], hi[1], f0, f1,
+                  c0, c1, lo[2], hi[2], g0, g1, d0, d1, lo[3], hi[3], h0, h1);
+    uint32_t i0, i1, j0, j1, k0, k1, l0, l1;  // x4 of the four
+    glasm::mul_x4(a0, a1, a0, a1, i0, i1, b0, b1, b0, b1, j0, j1,
+                  c0, c1, c0, c1, k0, k1, d0, d1, d0, d1, l0, l1);
+    glasm::mul_x4(e0, e1, i0, i1, lo[0], hi[0], f0, f1, j0, j1, lo[1], hi[1],
+                  g0, g1, k0, k1, lo[2], hi[2], h0, h1, l0, l1, lo[3], hi[3]);
 }
 
-__device__ __forceinline__ W w_shl(W a, int k) {  // a * 2^k, k small (1..2)
-    uint64_t lo = a.lo << k;
-    uint32_t hi = (a.hi << k) | (uint32_t)(a.lo >> (64 - k));
-    return W{lo, hi};
+__device__ __forceinline__ void sbox_x1(uint32_t& lo, uint32_t& hi) {
+    uint32_t a0, a1, e0, e1, i0, i1;
+    glasm::mul_x1(lo, hi, lo, hi, a0, a1);
+    glasm::mul_x2(a0, a1, lo, hi, e0, e1, a0, a1, a0, a1, i0, i1);
+    glasm::mul_x1(e0, e1, i0, i1, lo, hi);
 }
 
-// lo + hi * 2^64 mod p, hi < 2^32: 2^64 = EPS (mod p).
-__device__ __forceinline__ uint64_t w_reduce(W a) {
-    uint64_t t1 = ((uint64_t)a.hi << 32) - a.hi;  // hi * EPS < 2^64
-    uint64_t t2 = a.lo + t1;
-    return t2 + (t2 < a.lo ? gl::EPS : 0);
-}
-
-// M4 block (suggested_mds.rs block_mul) on wide values.
-__device__ __forceinline__ void m4(W& x0, W& x1, W& x2, W& x3) {
-    W t0 = w_add(x0, x1);
-    W t1 = w_add(x2, x3);
-    W t2 = w_add(w_shl(x1, 1), t1);
-    W t3 = w_add(w_shl(x3, 1), t0);
-    W t4 = w_add(w_shl(t1, 2), t3);
-    W t5 = w_add(w_shl(t0, 2), t2);
-    W t6 = w_add(t3, t5);
-    W t7 = w_add(t2, t4);
+// Limb form of the external MDS (suggested_mds_mul) applied to (lo, hi): outputs L[i], H[i]
+// with L, H < 64 * 2^32.
+__device__ __forceinline__ void m4_limbs(uint64_t& x0, uint64_t& x1, uint64_t& x2, uint64_t& x3) {
+    uint64_t t0 = x0 + x1;
+    uint64_t t1 = x2 + x3;
+    uint64_t t2 = (x1 << 1) + t1;
+    uint64_t t3 = (x3 << 1) + t0;
+    uint64_t t4 = (t1 << 2) + t3;
+    uint64_t t5 = (t0 << 2) + t2;
+    uint64_t t6 = t3 + t5;
+    uint64_t t7 = t2 + t4;
     x0 = t6; x1 = t5; x2 = t7; x3 = t4;
 }
 
-// External MDS: coefficients are <= 64 in row sum, so the wide sums stay < 2^71.
-__device__ __forceinline__ void mds_ext(uint64_t s[12]) {
-    W x[12];
+__device__ __forceinline__ void mds_ext_limbs(const uint32_t* v, uint64_t* X) {
 #pragma unroll
-    for (int i = 0; i < 12; i++) x[i] = w_of(s[i]);
-    m4(x[0], x[1], x[2], x[3]);
-    m4(x[4], x[5], x[6], x[7]);
-    m4(x[8], x[9], x[10], x[11]);
+    for (int i = 0; i < 12; i++) X[i] = v[i];
+    m4_limbs(X[0], X[1], X[2], X[3]);
+    m4_limbs(X[4], X[5], X[6], X[7]);
+    m4_limbs(X[8], X[9], X[10], X[11]);
 #pragma unroll
     for (int i = 0; i < 4; i++) {
-        W a = x[i], b = x[i + 4], c = x[i + 8];
-        W sum = w_add(w_add(a, b), c);
-        s[i] = w_reduce(w_add(sum, a));
-        s[i + 4] = w_reduce(w_add(sum, b));
-        s[i + 8] = w_reduce(w_add(sum, c));
+        uint64_t a = X[i], b = X[i + 4], c = X[i + 8];
+        uint64_t s = a + b + c;
+        X[i] = s + a;
+        X[i + 4] = s + b;
+        X[i + 8] = s + c;
     }
 }
 
-__device__ __forceinline__ uint64_t sbox(uint64_t x) {  // x^7, state_generic_impl.rs:141-147
-    uint64_t x2 = gl::mul(x, x);
-    uint64_t x3 = gl::mul(x2, x);
-    uint64_t x4 = gl::mul(x2, x2);
-    return gl::mul(x4, x3);
+// (L, H) -> reduced (lo, hi) for all 12 elements.
+__device__ __forceinline__ void reduce12(const uint64_t* L, const uint64_t* H, uint32_t* lo, uint32_t* hi) {
+#pragma unroll
+    for (int q = 0; q < 3; q++) {
+        const int i = 4 * q;
+        glasm::reduce_x4(L[i], (uint32_t)H[i], (uint32_t)(H[i] >> 32), lo[i], hi[i],
+                         L[i + 1], (uint32_t)H[i + 1], (uint32_t)(H[i + 1] >> 32), lo[i + 1], hi[i + 1],
+                         L[i + 2], (uint32_t)H[i + 2], (uint32_t)(H[i + 2] >> 32), lo[i + 2], hi[i + 2],
+                         L[i + 3], (uint32_t)H[i + 3], (uint32_t)(H[i + 3] >> 32), lo[i + 3], hi[i + 3]);
+    }
 }
 
-__device__ __forceinline__ void mds_int(uint64_t s[12]) {
-    constexpr int SH[12] = {4, 14, 11, 8, 0, 5, 2, 9, 13, 6, 3, 12};
-    W sum = w_of(s[0]);
-#pragma unroll
-    for (int i = 1; i < 12; i++) sum = w_add(sum, w_of(s[i]));
-    // s_i * 2^sh_i + sum: (lo, hi) with hi < 2^14 + 12, reduced once.
+// Full round r on the pending limbs (L, H) of the state (the external MDS of the previous
+// step not yet reduced): reduce(L + RC_r, H + RC_r), x^7, then the external MDS into
+// new pending limbs.  Leaves the reduced S-box output in s.
+__device__ __forceinline__ void full_round(State& s, uint64_t* L, uint64_t* H, int r) {
 #pragma unroll
     for (int i = 0; i < 12; i++) {
-        W v;
-        if (SH[i] == 0) {
-            v = w_of(s[i]);
-        } else {
-            v.lo = s[i] << SH[i];
-            v.hi = (uint32_t)(s[i] >> (64 - SH[i]));
-        }
-        s[i] = w_reduce(w_add(v, sum));
+        L[i] += RCL.lo[r][i];
+        H[i] += RCL.hi[r][i];
     }
+    reduce12(L, H, s.lo, s.hi);
+#pragma unroll
+    for (int q = 0; q < 3; q++) sbox_x4(s.lo + 4 * q, s.hi + 4 * q);
+    mds_ext_limbs(s.lo, L);
+    mds_ext_limbs(s.hi, H);
 }
 
-__device__ __forceinline__ void permute(uint64_t s[12]) {
-    mds_ext(s);
-#pragma unroll
-    for (int r = 0; r < 4; r++) {
-#pragma unroll
-        for (int i = 0; i < 12; i++) s[i] = sbox(gl::add(s[i], RC[r][i]));
-        mds_ext(s);
+// One partial round on a reduced state: s0 += RC, s0 = s0^7, then M_I.
+__device__ __forceinline__ void partial_round(State& s, int r) {
+    {
+        uint64_t L0 = (uint64_t)s.lo[0] + RCL.lo[r][0];
+        uint64_t H0 = (uint64_t)s.hi[0] + RCL.hi[r][0];
+        glasm::reduce_x1(L0, (uint32_t)H0, (uint32_t)(H0 >> 32), s.lo[0], s.hi[0]);
+        sbox_x1(s.lo[0], s.hi[0]);
     }
+    glasm::mi_layer(s.lo, s.hi);
+}
+
+// The permutation (state_generic_impl.rs:221-236): MDS; 4 x (RC, S-box, MDS);
+// 22 partial rounds; 4 x (RC, S-box, MDS).
+__device__ __forceinline__ void permute(State& s) {
+    uint64_t L[12], H[12];
+    mds_ext_limbs(s.lo, L);
+    mds_ext_limbs(s.hi, H);
+#pragma unroll 1
+    for (int r = 0; r < 4; r++) full_round(s, L, H, r);
+    reduce12(L, H, s.lo, s.hi);
+#pragma unroll 1
+    for (int r = 4; r < 26; r++) partial_round(s, r);
 #pragma unroll
-    for (int r = 4; r < 26; r++) {
-        s[0] = sbox(gl::add(s[0], RC[r][0]));
-        mds_int(s);
+    for (int i = 0; i < 12; i++) {
+        L[i] = s.lo[i];
+        H[i] = s.hi[i];
     }
+#pragma unroll 1
+    for (int r = 26; r < 30; r++) full_round(s, L, H, r);
+    reduce12(L, H, s.lo, s.hi);
+}
+
+__device__ __forceinline__ void permute(uint64_t v[12]) {
+    State s;
 #pragma unroll
-    for (int r = 26; r < 30; r++) {
-#pragma unroll
-        for (int i = 0; i < 12; i++) s[i] = sbox(gl::add(s[i], RC[r][i]));
-        mds_ext(s);
+    for (int i = 0; i < 12; i++) {
+        s.lo[i] = (uint32_t)v[i];
+        s.hi[i] = (uint32_t)(v[i] >> 32);
     }
+    permute(s);
+#pragma unroll
+    for (int i = 0; i < 12; i++) v[i] = ((uint64_t)s.hi[i] << 32) | s.lo[i];
 }
 
 }  // namespace p2

@@ -147,6 +147,12 @@ int bj_lde_commit_h(const uint64_t* trace_h, uint32_t n_cols, uint32_t log_n, ui
 
 /* ------------------------------------------------------------- utility */
 
+/* Batched field arithmetic through the device field layer (utility for parity tests of
+ * the Goldilocks primitives, field/goldilocks/mod.rs:186-325): out[i] = canonical(a[i] op b[i]),
+ * op 0 = mul, 1 = add, 2 = sub, 3 = a + b * 2^32 (a < 2^63, b < 2^63 with b >> 32 < 2^31),
+ * 4 = canonical(a).  Device pointers. */
+int bj_gl_op_d(int op, const uint64_t* a, const uint64_t* b, uint64_t* out, size_t n, void* stream);
+
 /* Bench/test input (not a reference entry point): column-major synthetic trace,
  * x = splitmix64(seed + (first_col + c) * n + r) reduced once mod p. */
 int bj_fill_synthetic_d(uint64_t* dst, uint32_t n_cols, size_t col_stride, uint32_t log_n, uint64_t seed,

@@ -1,0 +1,304 @@
+#!/usr/bin/env python3
+"""Generate era-boojum_amd/csrc/gl_asm.hpp: gfx950 inline-asm Goldilocks primitives.
+
+Why asm: on gfx950 every carry-producing / 64-bit / multiply VALU op issues at half
+rate while 32-bit logic is full rate (tools/microbench_isa.hip), so the multiply is
+priced by its instruction count.  hipcc materialises carries through v_cmp_lt_u64 +
+v_cndmask + v_mov pairs (~31 instructions per multiply); the sequences
+below keep every carry in an SGPR pair and use 14 instructions per multiply.
+
+Each primitive is emitted in N-way interleaved forms (N independent operations,
+round-robin) so a carry consumer sits >= 2 instructions after its producer: gfx950
+needs 2 wait states between a VALU write of an SGPR and a VALU read of it (hipcc pads
+exactly that).  Where the interleave leaves fewer, the generator inserts s_nop.
+
+Scratch: fixed VGPR pairs v[0:K) and SGPR pairs s[40:66) are declared clobbered; all
+other operands are compiler-allocated 32-bit registers (no 64-bit operand halves are
+ever needed, which inline asm cannot address).
+
+Field semantics: p = 2^64 - 2^32 + 1, EPS = 2^32 - 1; inputs any u64, outputs any u64
+representative of the right residue (never canonicalised here).
+"""
+import os
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+OUT = os.path.join(ROOT, "era-boojum_amd", "csrc", "gl_asm.hpp")
+
+SGPR_BASE = 40
+
+
+def sp(i):
+    return "s[%d:%d]" % (SGPR_BASE + 2 * i, SGPR_BASE + 2 * i + 1)
+
+
+JUNK = sp(12)  # carry-out sink (never read)
+
+
+class Stream:
+    """One operation's instruction list; operands as format fields."""
+
+    def __init__(self, instrs):
+        self.instrs = instrs  # list of (text, reads_sgprs set, writes_sgprs set)
+
+
+def mul_stream(k, vbase):
+    """z = a * b mod p in 14 instructions.  Inputs a0,a1,b0,b1; outputs z0,z1.
+    Scratch pairs P,U,W,V at vbase..vbase+7, m at vbase+8; carries cA, cB, cW.
+
+    a*b = P + (a0 b1 + a1 b0) 2^32 + V 2^64 with P = a0 b0, V = a1 b1.  The cross sum is
+    one mad, W = a0 b1 + U (U = a1 b0), whose carry-out cw is worth 2^96 = 2^32 * 2^64,
+    i.e. it adds to the top word r3.  Columns: r0 = P0, r1 = P1 + W0, r2 = W1 + V0 + c,
+    r3 = V1 + cw + c'.  Reduction (2^64 = EPS, 2^96 = -1): x = (r1:r0) - r3 with borrow B
+    (r3's own carry c' enters as the borrow-in), r2' = r2 - B (borrow B2),
+    z = r2' * EPS + x, + EPS on overflow, + B2 (the r2 = 0, B = 1 case, where r2 - B wraps
+    to 2^32 - 1 and the product is short by exactly one)."""
+    P0, P1, U0, U1, W0, W1, V0, V1, M = ["v%d" % (vbase + i) for i in range(9)]
+    P, U, W, V = ["v[%d:%d]" % (vbase + 2 * i, vbase + 2 * i + 1) for i in range(4)]
+    cA, cB, cW = sp(3 * k), sp(3 * k + 1), sp(3 * k + 2)
+    a0, a1, b0, b1, z0, z1 = ["%%[%s%d]" % (n, k) for n in ("a0", "a1", "b0", "b1", "z0", "z1")]
+    I = []
+    I.append(("v_mad_u64_u32 %s, %s, %s, %s, 0" % (U, JUNK, a1, b0), set(), {JUNK}))
+    I.append(("v_mad_u64_u32 %s, %s, %s, %s, 0" % (P, JUNK, a0, b0), set(), {JUNK}))
+    I.append(("v_mad_u64_u32 %s, %s, %s, %s, %s" % (W, cW, a0, b1, U), set(), {cW}))
+    I.append(("v_mad_u64_u32 %s, %s, %s, %s, 0" % (V, JUNK, a1, b1), set(), {JUNK}))
+    I.append(("v_add_co_u32 %s, %s, %s, %s" % (P1, cA, P1, W0), set(), {cA}))            # r1
+    I.append(("v_addc_co_u32 %s, %s, %s, 0, %s" % (V1, JUNK, V1, cW), {cW}, {JUNK}))     # V1 + cw
+    I.append(("v_addc_co_u32 %s, %s, %s, %s, %s" % (W1, cB, W1, V0, cA), {cA}, {cB}))    # r2, c'
+    I.append(("v_subb_co_u32 %s, %s, %s, %s, %s" % (P0, cA, P0, V1, cB), {cB}, {cA}))    # r0 - r3
+    I.append(("v_subb_co_u32 %s, %s, %s, 0, %s" % (P1, cA, P1, cA), {cA}, {cA}))         # B
+    I.append(("v_subb_co_u32 %s, %s, %s, 0, %s" % (W1, cA, W1, cA), {cA}, {cA}))         # r2', B2
+    I.append(("v_mad_u64_u32 %s, %s, %s, -1, %s" % (U, cB, W1, P), set(), {cB}))         # C
+    I.append(("v_cndmask_b32_e64 %s, 0, -1, %s" % (M, cB), {cB}, set()))
+    I.append(("v_addc_co_u32 %s, %s, %s, %s, %s" % (z0, cB, U0, M, cA), {cA}, {cB}))
+    I.append(("v_addc_co_u32 %s, %s, %s, 0, %s" % (z1, JUNK, U1, cB), {cB}, {JUNK}))
+    return I
+
+
+def reduce_stream(k, vbase):
+    """z = L + H * 2^32 mod p for a 64-bit pair L and H = (Hhi:Hlo) given as two 32-bit
+    operands, with L < 2^63 and Hhi < 2^31 (so Hhi * EPS + L < 2^64).  These bounds hold
+    for every lazily accumulated linear-layer limb in poseidon2.hpp (< 2^48).
+    Scratch pair W at vbase, m at vbase+2."""
+    W = "v[%d:%d]" % (vbase, vbase + 1)
+    W0, W1, M = "v%d" % vbase, "v%d" % (vbase + 1), "v%d" % (vbase + 2)
+    cA = sp(2 * k)
+    L, Hlo, Hhi, z0, z1 = ["%%[%s%d]" % (n, k) for n in ("L", "Hlo", "Hhi", "z0", "z1")]
+    I = []
+    # value = L + Hlo*2^32 + Hhi*2^64 == (Hhi*EPS + L) + Hlo*2^32
+    I.append(("v_mad_u64_u32 %s, %s, %s, -1, %s" % (W, JUNK, Hhi, L), set(), {JUNK}))
+    I.append(("v_add_co_u32 %s, %s, %s, %s" % (W1, cA, W1, Hlo), set(), {cA}))
+    # a carry out of the high word is 2^64 == EPS; W then < 2^48 so W + EPS cannot overflow
+    I.append(("v_cndmask_b32_e64 %s, 0, -1, %s" % (M, cA), {cA}, set()))
+    I.append(("v_add_co_u32 %s, %s, %s, %s" % (z0, cA, W0, M), set(), {cA}))
+    I.append(("v_addc_co_u32 %s, %s, %s, 0, %s" % (z1, JUNK, W1, cA), {cA}, {JUNK}))
+    return I
+
+
+def addsub_stream(k, vbase, op):
+    """z = a +/- b mod p for any u64 a, b (a0,a1,b0,b1 -> z0,z1)."""
+    M = "v%d" % vbase
+    cA = sp(2 * k)
+    a0, a1, b0, b1, z0, z1 = ["%%[%s%d]" % (n, k) for n in ("a0", "a1", "b0", "b1", "z0", "z1")]
+    I = []
+    if op == "add":
+        # a + b = s + c*2^64 == s + c*EPS; a second overflow can only follow the first
+        I.append(("v_add_co_u32 %s, %s, %s, %s" % (z0, cA, a0, b0), set(), {cA}))
+        I.append(("v_addc_co_u32 %s, %s, %s, %s, %s" % (z1, cA, a1, b1, cA), {cA}, {cA}))
+        for _ in range(2):
+            I.append(("v_cndmask_b32_e64 %s, 0, -1, %s" % (M, cA), {cA}, set()))
+            I.append(("v_add_co_u32 %s, %s, %s, %s" % (z0, cA, z0, M), set(), {cA}))
+            I.append(("v_addc_co_u32 %s, %s, %s, 0, %s" % (z1, cA, z1, cA), {cA}, {cA}))
+    else:
+        # a - b = d - c*2^64 == d - c*EPS
+        I.append(("v_sub_co_u32 %s, %s, %s, %s" % (z0, cA, a0, b0), set(), {cA}))
+        I.append(("v_subb_co_u32 %s, %s, %s, %s, %s" % (z1, cA, a1, b1, cA), {cA}, {cA}))
+        for _ in range(2):
+            I.append(("v_cndmask_b32_e64 %s, 0, -1, %s" % (M, cA), {cA}, set()))
+            I.append(("v_sub_co_u32 %s, %s, %s, %s" % (z0, cA, z0, M), set(), {cA}))
+            I.append(("v_subb_co_u32 %s, %s, %s, 0, %s" % (z1, cA, z1, cA), {cA}, {cA}))
+    return I
+
+
+def canon_stream(k, vbase):
+    """z = canonical(x): x + EPS overflows iff x >= p, and then x + EPS - 2^64 = x - p."""
+    T0, T1 = "v%d" % vbase, "v%d" % (vbase + 1)
+    cA = sp(2 * k)
+    a0, a1, z0, z1 = ["%%[%s%d]" % (n, k) for n in ("a0", "a1", "z0", "z1")]
+    I = []
+    I.append(("v_add_co_u32 %s, %s, %s, -1" % (T0, cA, a0), set(), {cA}))
+    I.append(("v_addc_co_u32 %s, %s, %s, 0, %s" % (T1, cA, a1, cA), {cA}, {cA}))
+    I.append(("v_cndmask_b32_e64 %s, %s, %s, %s" % (z0, a0, T0, cA), {cA}, set()))
+    I.append(("v_cndmask_b32_e64 %s, %s, %s, %s" % (z1, a1, T1, cA), {cA}, set()))
+    return I
+
+
+def merge(streams):
+    merged = []
+    idx = [0] * len(streams)
+    while any(i < len(s) for i, s in zip(idx, streams)):
+        for j, s in enumerate(streams):
+            if idx[j] < len(s):
+                merged.append(s[idx[j]])
+                idx[j] += 1
+    return merged
+
+
+def interleave(streams):
+    """Round-robin merge, then pad SGPR write->read distances to >= 2 wait states."""
+    return pad(merge(streams))
+
+
+def pad(merged):
+    out = []
+    last_write = {}  # sgpr -> position in out (counting only instructions)
+    pos = 0
+    for text, reads, writes in merged:
+        need = 0
+        for r in reads:
+            if r in last_write:
+                gap = pos - last_write[r] - 1  # instructions in between
+                need = max(need, 2 - gap)
+        if need > 0:
+            out.append("s_nop %d" % (need - 1))
+            pos += need
+        out.append(text)
+        for w in writes:
+            last_write[w] = pos
+        pos += 1
+    return out
+
+
+def emit_fn(name, n, stream_fn, vper, in_names, out_names, in_kinds=None, doc=""):
+    streams = [stream_fn(k, vper * k) for k in range(n)]
+    body = interleave(streams)
+    n_v = vper * n
+    args = []
+    for k in range(n):
+        for nm in in_names:
+            kind = (in_kinds or {}).get(nm, "uint32_t")
+            args.append("%s %s%d" % (kind, nm, k))
+        for nm in out_names:
+            args.append("uint32_t& %s%d" % (nm, k))
+    outs = ", ".join('[%s%d] "=&v"(%s%d)' % (nm, k, nm, k) for k in range(n) for nm in out_names)
+    ins = ", ".join('[%s%d] "v"(%s%d)' % (nm, k, nm, k) for k in range(n) for nm in in_names)
+    clob = ['"v%d"' % i for i in range(n_v)] + ['"s%d"' % i for i in range(SGPR_BASE, SGPR_BASE + 26)]
+    lines = []
+    if doc:
+        lines.append("// " + doc)
+    lines.append("__device__ __forceinline__ void %s(%s) {" % (name, ", ".join(args)))
+    lines.append("    asm volatile(")
+    for t in body:
+        lines.append('        "%s\\n"' % t)
+    lines.append("        : %s" % outs)
+    lines.append("        : %s" % ins)
+    lines.append("        : %s);" % ", ".join(clob))
+    lines.append("}")
+    return "\n".join(lines) + "\n"
+
+
+SH = [4, 14, 11, 8, 0, 5, 2, 9, 13, 6, 3, 12]  # M_I diagonal exponents, state_generic_impl.rs:71-84
+
+
+def emit_mi_layer():
+    """Partial-round internal linear layer on a reduced state (lo[i], hi[i] 32-bit):
+    s_i' = s_i * 2^SH[i] + sum_j s_j  (M_I = diag(2^SH) + 1 1^T, state_generic_impl.rs:166-202).
+    Limb form: Ls = sum lo_j, Hs = sum hi_j (mad chains, no zero-extension), then per element
+    L = lo_i * 2^k + Ls, H = hi_i * 2^k + Hs (one mad each; < 2^47) and the 5-instruction
+    limb reduction.  One asm block, 12 elements reduced 4 at a time."""
+    SUM = {("L", c): "v[%d:%d]" % (2 * c, 2 * c + 1) for c in range(3)}
+    SUM.update({("H", c): "v[%d:%d]" % (6 + 2 * c, 7 + 2 * c) for c in range(3)})
+    consts = {}
+    sreg = SGPR_BASE + 26
+    pro = []
+    for k in sorted(set(SH)):
+        if k > 6:
+            consts[k] = "s%d" % sreg
+            pro.append(("s_mov_b32 s%d, %d" % (sreg, 1 << k), set(), set()))
+            sreg += 1
+    chains = []
+    for limb, src in (("L", "lo"), ("H", "hi")):
+        for c in range(3):
+            ch = []
+            for t in range(4):
+                i = 4 * c + t
+                acc = SUM[(limb, c)]
+                ch.append(("v_mad_u64_u32 %s, %s, %%[%s%d], 1, %s" % (acc, JUNK, src, i, "0" if t == 0 else acc),
+                           set(), {JUNK}))
+            chains.append(ch)
+    body = pro + merge(chains)
+    for limb in ("L", "H"):
+        a = SUM[(limb, 0)]
+        body.append(("v_lshl_add_u64 %s, %s, 0, %s" % (a, SUM[(limb, 1)], a), set(), set()))
+        body.append(("v_lshl_add_u64 %s, %s, 0, %s" % (a, SUM[(limb, 2)], a), set(), set()))
+    Ls, Hs = SUM[("L", 0)], SUM[("H", 0)]
+    for g in range(3):
+        streams = []
+        for j in range(4):
+            i = 4 * g + j
+            base = 12 + 8 * j
+            Lp = "v[%d:%d]" % (base, base + 1)
+            Hp = "v[%d:%d]" % (base + 2, base + 3)
+            H0, H1 = "v%d" % (base + 2), "v%d" % (base + 3)
+            Wp = "v[%d:%d]" % (base + 4, base + 5)
+            W0, W1, M = "v%d" % (base + 4), "v%d" % (base + 5), "v%d" % (base + 6)
+            K = consts.get(SH[i], str(1 << SH[i]))
+            c = sp(j)
+            st = [
+                ("v_mad_u64_u32 %s, %s, %%[lo%d], %s, %s" % (Lp, JUNK, i, K, Ls), set(), {JUNK}),
+                ("v_mad_u64_u32 %s, %s, %%[hi%d], %s, %s" % (Hp, JUNK, i, K, Hs), set(), {JUNK}),
+                ("v_mad_u64_u32 %s, %s, %s, -1, %s" % (Wp, JUNK, H1, Lp), set(), {JUNK}),
+                ("v_add_co_u32 %s, %s, %s, %s" % (W1, c, W1, H0), set(), {c}),
+                ("v_cndmask_b32_e64 %s, 0, -1, %s" % (M, c), {c}, set()),
+                ("v_add_co_u32 %%[lo%d], %s, %s, %s" % (i, c, W0, M), set(), {c}),
+                ("v_addc_co_u32 %%[hi%d], %s, %s, 0, %s" % (i, JUNK, W1, c), {c}, {JUNK}),
+            ]
+            streams.append(st)
+        body += merge(streams)
+    text = pad(body)
+    # in place: element i's result overwrites lo[i]/hi[i] only after every read of them
+    # (the sums read all inputs first; element i's own mads read lo[i]/hi[i] before its write)
+    args = ", ".join(["uint32_t* lo", "uint32_t* hi"])
+    outs = ", ".join('[lo%d] "+v"(lo[%d]), [hi%d] "+v"(hi[%d])' % (i, i, i, i) for i in range(12))
+    ins = ""
+    clob = ['"v%d"' % i for i in range(12 + 32)] + ['"s%d"' % i for i in range(SGPR_BASE, sreg)]
+    lines = ["// Poseidon2 partial-round M_I on a reduced state (%d VALU instructions)" % sum(1 for t in text if t.startswith("v_")),
+             "__device__ __forceinline__ void mi_layer(%s) {" % args, "    asm volatile("]
+    lines += ['        "%s\\n"' % t for t in text]
+    lines += ["        : %s" % outs, "        : %s" % ins, "        : %s);" % ", ".join(clob), "}"]
+    return "\n".join(lines) + "\n"
+
+
+def main():
+    parts = ['''// GENERATED by tools/gen_gl_asm.py -- do not edit.
+// gfx950 inline-asm Goldilocks primitives (see the generator's docstring for the
+// design and the hazard rule).  p = 2^64 - 2^32 + 1.  All values are (lo, hi) 32-bit
+// halves of u64 representatives; results are NOT canonicalised.
+#pragma once
+#include <stdint.h>
+
+namespace glasm {
+''']
+    for n in (1, 2, 3, 4):
+        parts.append(emit_fn("mul_x%d" % n, n, mul_stream, 10, ["a0", "a1", "b0", "b1"], ["z0", "z1"],
+                             doc="%d independent products z = a * b mod p (14 instructions each)" % n))
+    for n in (1, 2, 3, 4):
+        parts.append(emit_fn("reduce_x%d" % n, n, reduce_stream, 4, ["L", "Hlo", "Hhi"], ["z0", "z1"],
+                             in_kinds={"L": "uint64_t"},
+                             doc="%d reductions z = L + (Hhi:Hlo) * 2^32 mod p, L and H < 2^63" % n))
+    for n in (1, 2, 4):
+        parts.append(emit_fn("add_x%d" % n, n, lambda k, vb: addsub_stream(k, vb, "add"), 2,
+                             ["a0", "a1", "b0", "b1"], ["z0", "z1"], doc="%d general additions" % n))
+        parts.append(emit_fn("sub_x%d" % n, n, lambda k, vb: addsub_stream(k, vb, "sub"), 2,
+                             ["a0", "a1", "b0", "b1"], ["z0", "z1"], doc="%d general subtractions" % n))
+    for n in (1, 2, 4):
+        parts.append(emit_fn("canon_x%d" % n, n, canon_stream, 2, ["a0", "a1"], ["z0", "z1"],
+                             doc="%d canonicalisations z = x mod p in [0, p)" % n))
+    parts.append(emit_mi_layer())
+    parts.append("}  // namespace glasm\n")
+    with open(OUT, "w") as f:
+        f.write("\n".join(parts))
+    print("wrote", OUT)
+
+
+if __name__ == "__main__":
+    main()
