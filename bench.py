@@ -203,7 +203,7 @@ class SingleGpu:
         ev = [torch.cuda.Event(enable_timing=True) for _ in range(4)] if timing else None
         if timing:
             ev[0].record()
-        call("bj_lde_d", self.trace.data_ptr(), n_cols, n, log_n, log_lde, ws.monomials.data_ptr(), ws.lde.data_ptr(),
+        call("bj_lde_d", self.trace.data_ptr(), n_cols, n, log_n, log_lde, ws.scratch.data_ptr(), ws.lde.data_ptr(),
              st)
         if timing:
             ev[1].record()

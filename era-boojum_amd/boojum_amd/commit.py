@@ -20,7 +20,7 @@ def _log2(n):
 class CommitWorkspace:
     """HBM buffers for a commit of n_cols x 2^log_n at LDE 2^log_lde, cap cap_size.
 
-    Sizes (bytes): monomials 8*C*n, lde 8*C*n*D, leaves 32*n*D, nodes 32*(n*D - cap)."""
+    Sizes (bytes): scratch 8*C*n, lde 8*C*n*D, leaves 32*n*D, nodes 32*(n*D - cap)."""
 
     def __init__(self, n_cols, log_n, log_lde, cap_size, device="cuda"):
         n, d = 1 << log_n, 1 << log_lde
@@ -29,7 +29,7 @@ class CommitWorkspace:
         if nl <= cap_size:
             raise ValueError("tree size must exceed cap size")
         self.n_cols, self.log_n, self.log_lde, self.cap_size = n_cols, log_n, log_lde, cap_size
-        self.monomials = torch.empty((n_cols, n), dtype=torch.int64, device=device)
+        self.scratch = torch.empty((n_cols, n), dtype=torch.int64, device=device)
         self.lde = torch.empty((n_cols, d, n), dtype=torch.int64, device=device)
         self.leaves = torch.empty((nl, 4), dtype=torch.int64, device=device)
         self.nodes = torch.empty((nl - cap_size, 4), dtype=torch.int64, device=device)
@@ -46,14 +46,14 @@ class CommitWorkspace:
 
 def witness_commit(trace, lde_degree, cap_size, workspace=None):
     """Commit a (C, n) int64 CUDA trace tensor.  Returns the workspace holding
-    monomials, lde (C, D, n), leaves, nodes and cap (all on device, canonical).
+    lde (C, D, n), leaves, nodes and cap (all on device, canonical).
     Asynchronous on the current stream."""
     v, c, n, stride = col_view(trace)
     log_n, log_d = _log2(n), _log2(lde_degree)
     ws = workspace or CommitWorkspace(c, log_n, log_d, cap_size, device=v.device)
     if (ws.n_cols, ws.log_n, ws.log_lde, ws.cap_size) != (c, log_n, log_d, cap_size):
         raise ValueError("workspace shape does not match the trace")
-    call("bj_lde_commit_d", v.data_ptr(), c, stride, log_n, log_d, cap_size, ws.monomials.data_ptr(),
+    call("bj_lde_commit_d", v.data_ptr(), c, stride, log_n, log_d, cap_size, ws.scratch.data_ptr(),
          ws.lde.data_ptr(), ws.leaves.data_ptr(), ws.nodes.data_ptr(), None, stream_of(v))
     return ws
 

@@ -29,20 +29,21 @@ def _log2(n):
     return n.bit_length() - 1
 
 
-def transform_raw_storages_to_lde(trace, lde_degree, monomials=None, out=None):
+def transform_raw_storages_to_lde(trace, lde_degree, scratch=None, out=None):
     """utils.rs:270-309 + transform_monomials_to_lde :311-403 for a (C, n) int64 CUDA
-    tensor.  Returns (monomials (C, n), lde (C, D, n)).  `monomials` / `out` may be
-    preallocated buffers (reused across calls by a batched prover)."""
+    tensor.  Returns lde (C, D, n) (the reference returns only the LDE storages; the
+    monomials are consumed).  `scratch` (C, n) / `out` may be preallocated buffers
+    (reused across calls by a batched prover)."""
     v, c, n, stride = col_view(trace)
     log_n, log_d = _log2(n), _log2(lde_degree)
     if log_d == 0:
         raise ValueError("lde_degree must be > 1 (utils.rs:283)")
-    if monomials is None:
-        monomials = torch.empty((c, n), dtype=torch.int64, device=v.device)
+    if scratch is None:
+        scratch = torch.empty((c, n), dtype=torch.int64, device=v.device)
     if out is None:
         out = torch.empty((c, lde_degree, n), dtype=torch.int64, device=v.device)
-    call("bj_lde_d", v.data_ptr(), c, stride, log_n, log_d, monomials.data_ptr(), out.data_ptr(), stream_of(v))
-    return monomials, out
+    call("bj_lde_d", v.data_ptr(), c, stride, log_n, log_d, scratch.data_ptr(), out.data_ptr(), stream_of(v))
+    return out
 
 
 def transform_monomials_to_lde(monomials, lde_degree, out=None):
@@ -83,14 +84,12 @@ class WitnessStorage:
     """WitnessStorage::from_base_trace (witness_storage.rs:18-116): the LDE of the
     variables/witness/multiplicity columns at `used_lde_degree`."""
 
-    def __init__(self, monomials, lde):
-        self.monomials = monomials
+    def __init__(self, lde):
         self.lde = lde
 
     @classmethod
     def from_base_trace(cls, trace, lde_degree):
-        mono, lde = transform_raw_storages_to_lde(trace, lde_degree)
-        return cls(mono, lde)
+        return cls(transform_raw_storages_to_lde(trace, lde_degree))
 
     def columns(self):
         return [ArcGenericLdeStorage(self.lde[c]) for c in range(self.lde.shape[0])]

@@ -27,7 +27,24 @@ hipError_t launch_synthetic(uint64_t* dst, size_t col_stride, uint32_t n_cols, u
 
 hipError_t launch_gl_op(int op, const uint64_t* a, const uint64_t* b, uint64_t* out, size_t n, hipStream_t st);
 
+hipError_t launch_twiddle_pyramid(uint64_t* out, uint32_t log_n, bool inverse, hipStream_t st);
+hipError_t launch_dif(uint64_t* dst, size_t dst_stride, const uint64_t* src, size_t src_stride, uint32_t n_cols,
+                      uint32_t log_n, const uint64_t* tw_pyr, bool canon_out, hipStream_t st);
+hipError_t launch_lde_forward(uint64_t* lde, size_t lde_col_stride, uint32_t n_cosets, const uint64_t* raw,
+                              size_t raw_stride, bool raw_bitrev, uint32_t n_cols, uint32_t log_n,
+                              const uint64_t* tw_pyr, const uint64_t* pw, size_t pw_stride, hipStream_t st);
+
 // power table sizes for a column of 2^log_n: lo 4096, hi max(1, n / 4096)
 inline size_t pw_hi_len(uint32_t log_n) { return log_n > 12 ? ((size_t)1 << (log_n - 12)) : 1; }
 
+}  // namespace bj
+
+namespace bj {
+// ntt_fast.hip: register-resident passes for 2^18 <= n <= 2^23
+bool fast_ntt_supported(uint32_t log_n);
+hipError_t launch_dif_fast(uint64_t* dst, size_t dst_stride, const uint64_t* src, size_t src_stride, uint32_t n_cols,
+                           uint32_t log_n, const uint64_t* tw_pyr, bool canon_out, hipStream_t st);
+hipError_t launch_lde_forward_fast(uint64_t* lde, size_t lde_col_stride, uint32_t n_cosets, const uint64_t* raw,
+                                   size_t raw_stride, bool raw_bitrev, uint32_t n_cols, uint32_t log_n,
+                                   const uint64_t* tw_pyr, const uint64_t* pw, size_t pw_stride, hipStream_t st);
 }  // namespace bj

@@ -43,7 +43,9 @@ inline hipStream_t S(void* s) { return reinterpret_cast<hipStream_t>(s); }
 struct Cache {
     std::mutex mu;
     std::map<std::tuple<int, uint32_t, int>, uint64_t*> tw;
+    std::map<std::tuple<int, uint32_t, int>, uint64_t*> pyr;
     std::map<std::tuple<int, uint32_t, uint64_t, uint64_t>, std::pair<uint64_t*, uint64_t*>> pw;
+    std::map<std::tuple<int, uint32_t, uint32_t, int>, uint64_t*> lde_pw;
 };
 Cache& cache() {
     static Cache* c = new Cache();
@@ -96,6 +98,61 @@ int get_powers(uint32_t log_n, uint64_t e_, uint64_t scale, const uint64_t** lo,
     return BJ_OK;
 }
 
+// DIF twiddle pyramid (ntt_dif.hip): n entries, TW[m/2 + j] = w_m^j.
+int get_pyramid(uint32_t log_n, bool inverse, const uint64_t** out) {
+    int dev = 0;
+    HIP_TRY(hipGetDevice(&dev), "hipGetDevice");
+    Cache& c = cache();
+    std::lock_guard<std::mutex> lk(c.mu);
+    auto key = std::make_tuple(dev, log_n, inverse ? 1 : 0);
+    auto it = c.pyr.find(key);
+    if (it != c.pyr.end()) { *out = it->second; return BJ_OK; }
+    const size_t n = (size_t)1 << log_n;
+    uint64_t* p = nullptr;
+    HIP_TRY(hipMalloc(&p, (n < 2 ? 2 : n) * sizeof(uint64_t)), "hipMalloc(pyramid)");
+    hipStream_t st;
+    HIP_TRY(hipStreamCreateWithFlags(&st, hipStreamNonBlocking), "hipStreamCreate");
+    hipError_t e = bj::launch_twiddle_pyramid(p, log_n, inverse, st);
+    if (e == hipSuccess) e = hipStreamSynchronize(st);
+    (void)hipStreamDestroy(st);
+    if (e != hipSuccess) { (void)hipFree(p); return hip_fail(e, "pyramid"); }
+    c.pyr[key] = p;
+    *out = p;
+    return BJ_OK;
+}
+
+uint64_t lde_coset(uint32_t log_n, uint32_t log_d, uint32_t i);
+
+// Power tables for all D cosets of an LDE: coset i at out + i * pw_stride, each
+// [lo 4096 | hi n/4096] for scale * s_i^j (scale = n^-1 when the source is the raw iNTT).
+int get_lde_powers(uint32_t log_n, uint32_t log_d, bool with_ninv, const uint64_t** out, size_t* stride) {
+    int dev = 0;
+    HIP_TRY(hipGetDevice(&dev), "hipGetDevice");
+    const size_t pstride = 4096 + bj::pw_hi_len(log_n);
+    *stride = pstride;
+    Cache& c = cache();
+    std::lock_guard<std::mutex> lk(c.mu);
+    auto key = std::make_tuple(dev, log_n, log_d, with_ninv ? 1 : 0);
+    auto it = c.lde_pw.find(key);
+    if (it != c.lde_pw.end()) { *out = it->second; return BJ_OK; }
+    const uint32_t D = 1u << log_d;
+    uint64_t* p = nullptr;
+    HIP_TRY(hipMalloc(&p, D * pstride * sizeof(uint64_t)), "hipMalloc(lde powers)");
+    hipStream_t st;
+    HIP_TRY(hipStreamCreateWithFlags(&st, hipStreamNonBlocking), "hipStreamCreate");
+    const uint64_t scale = with_ninv ? gl::canon(gl::inv((uint64_t)1 << log_n)) : 1;
+    hipError_t e = hipSuccess;
+    for (uint32_t i = 0; i < D && e == hipSuccess; i++)
+        e = bj::launch_power_tables(p + i * pstride, p + i * pstride + 4096, log_n, lde_coset(log_n, log_d, i), scale,
+                                    st);
+    if (e == hipSuccess) e = hipStreamSynchronize(st);
+    (void)hipStreamDestroy(st);
+    if (e != hipSuccess) { (void)hipFree(p); return hip_fail(e, "lde powers"); }
+    c.lde_pw[key] = p;
+    *out = p;
+    return BJ_OK;
+}
+
 inline bool is_pow2(size_t x) { return x && !(x & (x - 1)); }
 
 int log2_exact(size_t len, uint32_t* out) {
@@ -133,8 +190,8 @@ uint32_t bj_abi_version(void) { return (1u << 16) | 0u; }
 int bj_prepare(uint32_t log_n) {
     if (int r = check_log_n(log_n)) return r;
     const uint64_t* t;
-    if (int r = get_twiddles(log_n, false, &t)) return r;
-    if (int r = get_twiddles(log_n, true, &t)) return r;
+    if (int r = get_pyramid(log_n, false, &t)) return r;
+    if (int r = get_pyramid(log_n, true, &t)) return r;
     return BJ_OK;
 }
 
@@ -163,32 +220,33 @@ int bj_distribute_powers_d(uint64_t* cols, uint32_t n_cols, size_t col_stride, u
     return BJ_OK;
 }
 
+// The device transform is a DIF network over its own cached twiddle pyramid; a twiddle
+// pointer in the reference's format is accepted for signature parity and not read.
 int bj_fft_natural_to_bitreversed_d(uint64_t* cols, uint32_t n_cols, size_t col_stride, uint32_t log_n,
                                     uint64_t coset, const uint64_t* twiddles_d, void* stream) {
+    (void)twiddles_d;
     if (int r = check_log_n(log_n)) return r;
-    const uint64_t* tw = twiddles_d;
-    if (!tw && log_n > 0)
-        if (int r = get_twiddles(log_n, false, &tw)) return r;
-    const uint64_t *lo = nullptr, *hi = nullptr;
+    if (n_cols == 0) return BJ_OK;
     if (gl::canon(coset) != 1)
-        if (int r = get_powers(log_n, coset, 1, &lo, &hi)) return r;
-    HIP_TRY(bj::launch_ntt_nb(cols, col_stride, cols, col_stride, n_cols, log_n, tw, lo, hi, true, S(stream)),
-            "fft");
+        if (int r = bj_distribute_powers_d(cols, n_cols, col_stride, log_n, coset, stream)) return r;
+    const uint64_t* pyr;
+    if (int r = get_pyramid(log_n, false, &pyr)) return r;
+    HIP_TRY(bj::launch_dif(cols, col_stride, cols, col_stride, n_cols, log_n, pyr, true, S(stream)), "fft");
     return BJ_OK;
 }
 
 int bj_ifft_natural_to_natural_d(uint64_t* cols, uint32_t n_cols, size_t col_stride, uint32_t log_n,
                                  uint64_t coset, const uint64_t* inv_twiddles_d, void* stream) {
+    (void)inv_twiddles_d;
     if (int r = check_log_n(log_n)) return r;
     if (n_cols == 0) return BJ_OK;
-    const uint64_t* tw = inv_twiddles_d;
-    if (!tw && log_n > 0)
-        if (int r = get_twiddles(log_n, true, &tw)) return r;
     const size_t n = (size_t)1 << log_n;
-    // The bit-reversal is out of place; stage through a temporary of the same shape.
+    const uint64_t* pyr;
+    if (int r = get_pyramid(log_n, true, &pyr)) return r;
+    // inverse DIF (bit-reversed out) into a temporary, then bit-reverse * n^-1 back in place
     uint64_t* tmp = nullptr;
     HIP_TRY(hipMallocAsync((void**)&tmp, n * n_cols * 8, S(stream)), "hipMallocAsync");
-    hipError_t e = bj::launch_ntt_nb(tmp, n, cols, col_stride, n_cols, log_n, tw, nullptr, nullptr, false, S(stream));
+    hipError_t e = bj::launch_dif(tmp, n, cols, col_stride, n_cols, log_n, pyr, false, S(stream));
     const uint64_t n_inv = log_n ? gl::canon(gl::inv((uint64_t)n)) : 1;
     if (e == hipSuccess) e = bj::launch_bitrev_scale(cols, col_stride, tmp, n, n_cols, log_n, n_inv, S(stream));
     hipError_t e2 = hipFreeAsync(tmp, S(stream));
@@ -206,39 +264,38 @@ int bj_monomials_to_lde_d(const uint64_t* monomials, uint32_t n_cols, size_t mon
                           uint32_t log_lde, uint64_t* lde, void* stream) {
     if (int r = check_log_n(log_n + log_lde)) return r;
     if (log_lde == 0) return fail(BJ_EINVAL, "lde degree must be > 1 (utils.rs:283)");
+    if (n_cols == 0) return BJ_OK;
     const size_t n = (size_t)1 << log_n;
     const uint32_t D = 1u << log_lde;
-    const uint64_t* tw = nullptr;
-    if (log_n > 0)
-        if (int r = get_twiddles(log_n, false, &tw)) return r;
-    for (uint32_t i = 0; i < D; i++) {
-        const uint64_t *lo, *hi;
-        if (int r = get_powers(log_n, lde_coset(log_n, log_lde, i), 1, &lo, &hi)) return r;
-        HIP_TRY(bj::launch_ntt_nb(lde + (size_t)i * n, (size_t)D * n, monomials, mono_stride, n_cols, log_n, tw, lo,
-                                  hi, true, S(stream)),
-                "coset fft");
-    }
+    const uint64_t *pyr, *pw;
+    size_t pws;
+    if (int r = get_pyramid(log_n, false, &pyr)) return r;
+    if (int r = get_lde_powers(log_n, log_lde, false, &pw, &pws)) return r;
+    HIP_TRY(bj::launch_lde_forward(lde, (size_t)D * n, D, monomials, mono_stride, false, n_cols, log_n, pyr, pw, pws,
+                                   S(stream)),
+            "coset fft");
     return BJ_OK;
 }
 
 int bj_lde_d(const uint64_t* trace, uint32_t n_cols, size_t trace_stride, uint32_t log_n, uint32_t log_lde,
-             uint64_t* monomials, uint64_t* lde, void* stream) {
+             uint64_t* scratch, uint64_t* lde, void* stream) {
     if (int r = check_log_n(log_n + log_lde)) return r;
     if (log_lde == 0) return fail(BJ_EINVAL, "lde degree must be > 1 (utils.rs:283)");
     if (n_cols == 0) return BJ_OK;
     const size_t n = (size_t)1 << log_n;
     const uint32_t D = 1u << log_lde;
-    const uint64_t* itw = nullptr;
-    if (log_n > 0)
-        if (int r = get_twiddles(log_n, true, &itw)) return r;
-    // iFFT (utils.rs:295-304): CT with inverse twiddles into coset slot 0 of the LDE buffer
-    // (free scratch at this point), then bit-reverse * n^-1 into the monomial buffer.
-    HIP_TRY(bj::launch_ntt_nb(lde, (size_t)D * n, trace, trace_stride, n_cols, log_n, itw, nullptr, nullptr, false,
-                              S(stream)),
-            "ifft");
-    const uint64_t n_inv = log_n ? gl::canon(gl::inv((uint64_t)n)) : 1;
-    HIP_TRY(bj::launch_bitrev_scale(monomials, n, lde, (size_t)D * n, n_cols, log_n, n_inv, S(stream)), "bitrev");
-    return bj_monomials_to_lde_d(monomials, n_cols, n, log_n, log_lde, lde, stream);
+    const uint64_t *ipyr, *pyr, *pw;
+    size_t pws;
+    if (int r = get_pyramid(log_n, true, &ipyr)) return r;
+    if (int r = get_pyramid(log_n, false, &pyr)) return r;
+    if (int r = get_lde_powers(log_n, log_lde, true, &pw, &pws)) return r;
+    // iFFT (utils.rs:295-304) as an inverse DIF: scratch = n * monomials in bit-reversed
+    // order; the forward pass gathers it back in natural order and folds n^-1 into the
+    // coset powers (utils.rs:363-379), all D cosets per tile load.
+    HIP_TRY(bj::launch_dif(scratch, n, trace, trace_stride, n_cols, log_n, ipyr, false, S(stream)), "ifft");
+    HIP_TRY(bj::launch_lde_forward(lde, (size_t)D * n, D, scratch, n, true, n_cols, log_n, pyr, pw, pws, S(stream)),
+            "coset fft");
+    return BJ_OK;
 }
 
 int bj_fill_synthetic_d(uint64_t* dst, uint32_t n_cols, size_t col_stride, uint32_t log_n, uint64_t seed,
@@ -273,12 +330,12 @@ int bj_merkle_nodes_d(const uint64_t* leaves, size_t n_leaves, uint32_t cap_size
 }
 
 int bj_lde_commit_d(const uint64_t* trace, uint32_t n_cols, size_t trace_stride, uint32_t log_n, uint32_t log_lde,
-                    uint32_t cap_size, uint64_t* monomials, uint64_t* lde, uint64_t* leaves, uint64_t* nodes,
+                    uint32_t cap_size, uint64_t* scratch, uint64_t* lde, uint64_t* leaves, uint64_t* nodes,
                     uint64_t* cap_h, void* stream) {
     const size_t nl = (size_t)1 << (log_n + log_lde);
     if (!is_pow2(cap_size) || nl <= cap_size)
         return fail(BJ_EINVAL, "need power-of-two cap_size < n * D (merkle_tree.rs:83-96)");
-    if (int r = bj_lde_d(trace, n_cols, trace_stride, log_n, log_lde, monomials, lde, stream)) return r;
+    if (int r = bj_lde_d(trace, n_cols, trace_stride, log_n, log_lde, scratch, lde, stream)) return r;
     if (int r = bj_merkle_leaves_d(lde, n_cols, nl, nl, leaves, stream)) return r;
     if (int r = bj_merkle_nodes_d(leaves, nl, cap_size, nodes, stream)) return r;
     if (cap_h) {

@@ -88,13 +88,15 @@ int bj_ifft_natural_to_natural_h(uint64_t* col, size_t len, uint64_t coset);
  * driven by WitnessStorage::from_base_trace*, witness_storage.rs:18-116):
  *   monomials[c] = ifft_natural_to_natural(trace[c])
  *   lde[c][i]    = fft_natural_to_bitreversed(monomials[c], 7 * w_{nD}^{bitrev(i)})
- * trace:     n_cols columns of n = 2^log_n at trace + c * trace_stride (read only)
- * monomials: n_cols x n scratch/output, column c at monomials + c * n
- * lde:       n_cols x D x n, element (c, i, r) at lde + (c * D + i) * n + r
- *            (the reference's per-column Vec<coset> of ArcGenericLdeStorage)
+ * trace:   n_cols columns of n = 2^log_n at trace + c * trace_stride (read only)
+ * scratch: n_cols x n device workspace (on return it holds the raw inverse transform,
+ *          n * monomials in bit-reversed order -- an intermediate, like the reference's
+ *          consumed monomial vectors; bj_ifft_natural_to_natural_d gives monomials)
+ * lde:     n_cols x D x n, element (c, i, r) at lde + (c * D + i) * n + r
+ *          (the reference's per-column Vec<coset> of ArcGenericLdeStorage)
  * D = 2^log_lde. */
 int bj_lde_d(const uint64_t* trace, uint32_t n_cols, size_t trace_stride, uint32_t log_n,
-             uint32_t log_lde, uint64_t* monomials, uint64_t* lde, void* stream);
+             uint32_t log_lde, uint64_t* scratch, uint64_t* lde, void* stream);
 
 /* Coset LDE of already-monomial columns (transform_monomials_to_lde, utils.rs:311-403;
  * also the quotient commit path prover.rs:1471-1482).  monomials read only. */
@@ -135,7 +137,7 @@ int bj_merkle_nodes_d(const uint64_t* leaves, size_t n_leaves, uint32_t cap_size
  * the n*D rows, node levels to the cap.  All pointers device; cap additionally copied
  * to cap_h (host, cap_size x 4) if non-NULL (this synchronises the stream). */
 int bj_lde_commit_d(const uint64_t* trace, uint32_t n_cols, size_t trace_stride, uint32_t log_n,
-                    uint32_t log_lde, uint32_t cap_size, uint64_t* monomials, uint64_t* lde,
+                    uint32_t log_lde, uint32_t cap_size, uint64_t* scratch, uint64_t* lde,
                     uint64_t* leaves, uint64_t* nodes, uint64_t* cap_h, void* stream);
 
 /* Host-buffer variant (drop-in for a Rust prover that owns host Vecs): copies the trace

@@ -141,10 +141,14 @@ def test_host_seam_in_place(bj):
 def test_lde_batch(bj, c, log_n, log_d):
     x = rand((c, 1 << log_n), c * 100 + log_n)
     t = bj.field.to_device(x)
-    mono, l = bj.lde.transform_raw_storages_to_lde(t, 1 << log_d)
+    l = bj.lde.transform_raw_storages_to_lde(t, 1 << log_d)
     m_ref, l_ref = O.lde(x, log_d, threads=4)
-    eq(bj.field.to_host(mono), m_ref)
     eq(bj.field.to_host(l), l_ref)
+    # monomials path: iFFT natural->natural then monomials -> LDE
+    m = bj.field.to_device(x)
+    bj.fft.ifft_natural_to_natural(m, 1)
+    eq(bj.field.to_host(m), m_ref)
+    eq(bj.field.to_host(bj.lde.transform_monomials_to_lde(m, 1 << log_d)), l_ref)
 
 
 def test_lde_edge_columns(bj):
@@ -154,9 +158,8 @@ def test_lde_edge_columns(bj):
     x[2, 5] = 1
     x[3, :] = np.uint64(2**64 - 1)  # all non-canonical (== 2^32 - 2 mod p)
     t = bj.field.to_device(x)
-    mono, l = bj.lde.transform_raw_storages_to_lde(t, 4)
+    l = bj.lde.transform_raw_storages_to_lde(t, 4)
     m_ref, l_ref = O.lde(x, 2)
-    eq(bj.field.to_host(mono), m_ref)
     eq(bj.field.to_host(l), l_ref)
     assert not bj.field.to_host(l)[0].any()
 
@@ -167,7 +170,7 @@ def test_lde_with_strided_trace(bj):
     big = np.zeros((3, 3 << 11), dtype=np.uint64)
     big[:, : 1 << 11] = x
     t = bj.field.to_device(big)[:, : 1 << 11]
-    mono, l = bj.lde.transform_raw_storages_to_lde(t, 2)
+    l = bj.lde.transform_raw_storages_to_lde(t, 2)
     m_ref, l_ref = O.lde(x, 1)
     eq(bj.field.to_host(l), l_ref)
 
@@ -199,7 +202,6 @@ def test_witness_commit_matches_oracle(bj, c, log_n, log_d, cap):
     eq(bj.field.to_host(tr), tr_np)
     ws = bj.commit.witness_commit(tr, 1 << log_d, cap)
     ref = O.lde_commit(tr_np, log_d, cap, threads=8)
-    eq(bj.field.to_host(ws.monomials), ref["monomials"])
     eq(bj.field.to_host(ws.lde), ref["lde"])
     eq(bj.field.to_host(ws.leaves), ref["leaves"])
     eq(bj.field.to_host(ws.nodes), ref["nodes"])
