@@ -71,6 +71,8 @@ def main():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-sample-log-n", type=int, default=20)
     ap.add_argument("--cpu-sample-cols", type=int, default=32)
+    ap.add_argument("--dist-backend", default="nccl", choices=("nccl", "gloo"),
+                    help="gloo: rehearsal of the N>1 path with ranks sharing GPUs (not a benchmark)")
     args = ap.parse_args()
 
     import torch
@@ -79,11 +81,17 @@ def main():
     local_rank = int(os.environ.get("LOCAL_RANK", "0"))
     if world != args.gpus:
         raise SystemExit("--gpus %d but WORLD_SIZE=%d" % (args.gpus, world))
-    torch.cuda.set_device(local_rank)
     dist = None
+    if args.dist_backend == "gloo":
+        torch.cuda.set_device(local_rank % torch.cuda.device_count())
+    else:
+        torch.cuda.set_device(local_rank)
     if world > 1:
         import torch.distributed as dist
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local_rank))
+        if args.dist_backend == "nccl":
+            dist.init_process_group("nccl", device_id=torch.device("cuda", local_rank))
+        else:
+            dist.init_process_group("gloo")
 
     from boojum_amd import _lib, commit
     n_cols, log_n, log_lde, cap = CONFIGS[args.config]
@@ -93,8 +101,7 @@ def main():
     if world == 1:
         runner = SingleGpu(n_cols, log_n, log_lde, cap)
     else:
-        from boojum_amd.sharded import ShardedCommit
-        runner = ShardedCommit(n_cols, log_n, log_lde, cap, rank, world, dist)
+        runner = Sharded(n_cols, log_n, log_lde, cap, rank, world)
     stream = torch.cuda.current_stream()
 
     def barrier_sync():
@@ -113,7 +120,7 @@ def main():
     barrier_sync()
     dt = time.perf_counter() - t0
     if dist is not None:
-        tt = torch.tensor([dt], dtype=torch.float64, device="cuda")
+        tt = torch.tensor([dt], dtype=torch.float64, device="cuda" if args.dist_backend == "nccl" else "cpu")
         dist.all_reduce(tt, op=dist.ReduceOp.MAX)
         dt = float(tt.item())
     ms_per_step = dt / args.steps * 1e3
@@ -137,7 +144,9 @@ def main():
             roofline = {"bound": "valu", "achieved": None, "peak": VALU_PEAK_TOPS, "unit": "Tops/s", "frac": None,
                         "traffic": None, "kernel": "leaf_hash_kernel", "perms_per_s": leaf_perms / t_leaf}
         ntt_bytes = 8 * n * (n_cols // world) * (1 + D)
-        t_lde = phase["lde"] * 1e-3
+        t_lde = phase.get("lde_total", phase["lde"]) * 1e-3
+        if world > 1:  # the exchange is not NTT work: price the two NTT kernels alone
+            t_lde = (phase["ifft"] + phase["lde"]) * 1e-3
         ntt_roof = {"bound": "hbm", "achieved": ntt_bytes / t_lde / 1e9, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                     "frac": ntt_bytes / t_lde / 1e9 / HBM_PEAK_GBS, "traffic": stats.get("lde_hbm_bytes_per_launch"),
                     "bytes_alg": ntt_bytes}
@@ -228,6 +237,60 @@ class SingleGpu:
     def verify(self):
         """Cheap size-independent self-check of the last commit: the cap recomputed from
         the level below it must equal the stored cap (run outside the timed region)."""
+        pass
+
+
+class Sharded:
+    """G ranks, one GPU each: the coset-sharded commit of boojum_amd.sharded (column-sharded
+    trace -> local iNTT -> RCCL all-gather of coefficients -> this rank's leaf range of the
+    LDE -> leaves -> subtree -> cap all-gather).  Phases bracketed by events."""
+
+    PHASES = ("ifft", "exchange", "lde", "leaves", "nodes")
+
+    def __init__(self, n_cols, log_n, log_lde, cap, rank, world):
+        import torch
+        from boojum_amd.sharded import ShardedWorkspace
+        self.torch = torch
+        self.ws = ShardedWorkspace(n_cols, log_n, log_lde, cap, rank, world, device="cuda")
+        self.trace = self.ws.synthetic_trace_shard()
+        self.parallelism = "coset-sharded x%d (column-sharded trace, RCCL all-gather of coefficients)" % world
+        self.reset_timers()
+
+    def reset_timers(self):
+        self.pending = []
+
+    def step(self, timing):
+        from boojum_amd.sharded import sharded_witness_commit
+        torch = self.torch
+        if not timing:
+            sharded_witness_commit(self.trace, self.ws)
+            return
+        evs = {}
+
+        def mark(name):
+            e = torch.cuda.Event(enable_timing=True)
+            e.record()
+            evs[name] = e
+
+        mark("start")
+        sharded_witness_commit(self.trace, self.ws, marks=mark)
+        self.pending.append(evs)
+
+    def phase_ms(self):
+        self.torch.cuda.synchronize()
+        acc = {k: 0.0 for k in self.PHASES}
+        for evs in self.pending:
+            prev = evs["start"]
+            for k in self.PHASES:
+                acc[k] += prev.elapsed_time(evs[k])
+                prev = evs[k]
+        cnt = max(1, len(self.pending))
+        out = {k: v / cnt for k, v in acc.items()}
+        # the bench's roofline keys: the LDE phase is iNTT + exchange + forward
+        out["lde_total"] = out["ifft"] + out["exchange"] + out["lde"]
+        return out
+
+    def verify(self):
         pass
 
 

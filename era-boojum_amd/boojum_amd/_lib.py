@@ -31,6 +31,8 @@ SIGNATURES = {
     "bj_ifft_natural_to_natural_h": ([_u64p, _sz, _u64], _int),
     "bj_lde_d": ([_vp, _u32, _sz, _u32, _u32, _vp, _vp, _vp], _int),
     "bj_monomials_to_lde_d": ([_vp, _u32, _sz, _u32, _u32, _vp, _vp], _int),
+    "bj_lde_coeffs_d": ([_vp, _u32, _sz, _u32, _vp, _sz, _vp], _int),
+    "bj_lde_shard_d": ([_vp, _u32, _sz, _u32, _u32, _u32, _u32, _vp, _vp, _vp], _int),
     "bj_poseidon2_permute_d": ([_vp, _sz, _vp], _int),
     "bj_poseidon2_permute_h": ([_u64p], _int),
     "bj_hash_into_leaf_h": ([_u64p, _sz, _u64p], _int),

@@ -40,6 +40,11 @@ inline size_t pw_hi_len(uint32_t log_n) { return log_n > 12 ? ((size_t)1 << (log
 }  // namespace bj
 
 namespace bj {
+// shard.hip: sub-coset fold of the bit-reversed coefficients (G > D shards)
+constexpr uint32_t kMaxFold = 64;
+hipError_t launch_fold(uint64_t* dst, size_t dst_stride, const uint64_t* src, size_t src_stride, uint32_t n_cols,
+                       uint32_t log_m, uint32_t log_f, uint64_t s_pow_m, hipStream_t st);
+
 // ntt_fast.hip: register-resident passes for 2^18 <= n <= 2^23
 bool fast_ntt_supported(uint32_t log_n);
 hipError_t launch_dif_fast(uint64_t* dst, size_t dst_stride, const uint64_t* src, size_t src_stride, uint32_t n_cols,

@@ -298,6 +298,56 @@ int bj_lde_d(const uint64_t* trace, uint32_t n_cols, size_t trace_stride, uint32
     return BJ_OK;
 }
 
+int bj_lde_coeffs_d(const uint64_t* trace, uint32_t n_cols, size_t trace_stride, uint32_t log_n, uint64_t* coeffs,
+                    size_t coeffs_stride, void* stream) {
+    if (int r = check_log_n(log_n)) return r;
+    if (n_cols == 0) return BJ_OK;
+    const uint64_t* ipyr;
+    if (int r = get_pyramid(log_n, true, &ipyr)) return r;
+    HIP_TRY(bj::launch_dif(coeffs, coeffs_stride, trace, trace_stride, n_cols, log_n, ipyr, false, S(stream)), "ifft");
+    return BJ_OK;
+}
+
+int bj_lde_shard_d(const uint64_t* coeffs, uint32_t n_cols, size_t coeffs_stride, uint32_t log_n, uint32_t log_lde,
+                   uint32_t log_shards, uint32_t shard, uint64_t* work, uint64_t* lde, void* stream) {
+    if (int r = check_log_n(log_n + log_lde)) return r;
+    if (log_lde == 0) return fail(BJ_EINVAL, "lde degree must be > 1 (utils.rs:283)");
+    if (log_shards > log_n + log_lde) return fail(BJ_EINVAL, "more shards than leaves");
+    if (shard >= (1u << log_shards)) return fail(BJ_EINVAL, "shard index out of range");
+    if (n_cols == 0) return BJ_OK;
+    const size_t n = (size_t)1 << log_n;
+    const uint64_t* pyr;
+    if (log_shards <= log_lde) {
+        // whole cosets [P * D/G, (P+1) * D/G)
+        const uint32_t per = 1u << (log_lde - log_shards);
+        const uint64_t* pw;
+        size_t pws;
+        if (int r = get_pyramid(log_n, false, &pyr)) return r;
+        if (int r = get_lde_powers(log_n, log_lde, true, &pw, &pws)) return r;
+        HIP_TRY(bj::launch_lde_forward(lde, (size_t)per * n, per, coeffs, coeffs_stride, true, n_cols, log_n, pyr,
+                                       pw + (size_t)shard * per * pws, pws, S(stream)),
+                "coset fft");
+        return BJ_OK;
+    }
+    const uint32_t log_f = log_shards - log_lde;
+    if ((1u << log_f) > bj::kMaxFold) return fail(BJ_EINVAL, "G / D exceeds 64");
+    if (!work) return fail(BJ_EINVAL, "work buffer required when shards exceed the lde degree");
+    const uint32_t log_m = log_n - log_f;
+    const size_t m = (size_t)1 << log_m;
+    // s' = 7 * w_{nD}^{bitrev_{log G}(P)}; h_t = sum_a c_{t+am} (s'^m)^a (shard.hip)
+    const uint64_t g = gl::domain_generator(log_n + log_lde);
+    const uint64_t sp = gl::canon(gl::mul(gl::pow(g, gl::bitrev32(shard, log_shards)), gl::GENERATOR));
+    const uint64_t *lo, *hi;
+    const uint64_t scale = gl::canon(gl::inv((uint64_t)n));  // coeffs hold n * c_j
+    if (int r = get_pyramid(log_m, false, &pyr)) return r;
+    if (int r = get_powers(log_m, sp, scale, &lo, &hi)) return r;
+    HIP_TRY(bj::launch_fold(work, m, coeffs, coeffs_stride, n_cols, log_m, log_f, gl::pow(sp, m), S(stream)), "fold");
+    HIP_TRY(bj::launch_lde_forward(lde, m, 1, work, m, true, n_cols, log_m, pyr, lo, 4096 + bj::pw_hi_len(log_m),
+                                   S(stream)),
+            "coset fft");
+    return BJ_OK;
+}
+
 int bj_fill_synthetic_d(uint64_t* dst, uint32_t n_cols, size_t col_stride, uint32_t log_n, uint64_t seed,
                         uint64_t first_col, void* stream) {
     if (int r = check_log_n(log_n)) return r;

@@ -30,7 +30,6 @@ namespace bj {
 constexpr int DIF_THREADS = 256;
 constexpr int DIF_TILE_LOG = 13;
 constexpr int DIF_TILE = 1 << DIF_TILE_LOG;
-constexpr int DIF_PER_THREAD = DIF_TILE / DIF_THREADS;  // 32 elements, 16 butterflies per stage
 
 __device__ __forceinline__ void split(uint64_t x, uint32_t& lo, uint32_t& hi) {
     lo = (uint32_t)x;

@@ -103,6 +103,28 @@ int bj_lde_d(const uint64_t* trace, uint32_t n_cols, size_t trace_stride, uint32
 int bj_monomials_to_lde_d(const uint64_t* monomials, uint32_t n_cols, size_t mono_stride, uint32_t log_n,
                           uint32_t log_lde, uint64_t* lde, void* stream);
 
+/* ------------------------------------------------ coset-sharded LDE (8(e)) */
+/* The multi-GPU split of transform_raw_storages_to_lde (utils.rs:270-403) over G = 2^log_shards
+ * ranks: the flat leaf domain L = coset * n + row (merkle_tree.rs:112-157 leaf order) is cut
+ * into G contiguous ranges of m = n*D/G leaves; rank P owns [P*m, (P+1)*m).
+ *
+ * Step 1 (every rank, its own trace columns): bj_lde_coeffs_d writes the inverse transform
+ *   in the exchange format: column c holds n * c_j at position bitrev_n(j), where c_j are the
+ *   monomials of ifft_natural_to_natural (utils.rs:295-304).  Ranks all-gather these columns.
+ * Step 2 (every rank, all columns): bj_lde_shard_d evaluates its leaf range:
+ *   G <= D: cosets [P*D/G, (P+1)*D/G), each as in bj_lde_d;
+ *   G >  D: rows [q*m, (q+1)*m) of coset i = P / (G/D), q = P mod (G/D), as an m-point coset
+ *           FFT of the coefficients folded mod Y^m - s'^m, s' = 7 * w_{nD}^{bitrev_{log G}(P)}.
+ *   lde: n_cols x m, element (c, L - P*m) at lde + c * m + (L - P*m), identical to the slice
+ *   of bj_lde_d's output for those leaves.  work: n_cols x m device scratch (G > D only;
+ *   may be NULL when G <= D).  Requires log_shards <= log_n + log_lde and, for G > D,
+ *   G / D <= 64. */
+int bj_lde_coeffs_d(const uint64_t* trace, uint32_t n_cols, size_t trace_stride, uint32_t log_n,
+                    uint64_t* coeffs, size_t coeffs_stride, void* stream);
+int bj_lde_shard_d(const uint64_t* coeffs, uint32_t n_cols, size_t coeffs_stride, uint32_t log_n,
+                   uint32_t log_lde, uint32_t log_shards, uint32_t shard, uint64_t* work, uint64_t* lde,
+                   void* stream);
+
 /* ---------------------------------------------------------- Poseidon2 / Merkle */
 
 /* poseidon2_permutation (implementations/poseidon2/state_generic_impl.rs:221-249) on

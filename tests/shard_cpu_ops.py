@@ -1,0 +1,55 @@
+"""CPU stand-in for boojum_amd.sharded.HipShardOps, built on the oracle -- TEST ONLY.
+
+Lets the multi-process (gloo) tests exercise the sharded orchestration (column shards,
+all-gather order, leaf-range ownership, cap assembly incl. cap < G) on CPU tensors.
+Each step restates the same contract as the C-ABI entry point it stands in for
+(include/boojum_mi355x.h: bj_lde_coeffs_d, bj_lde_shard_d, bj_merkle_*_d)."""
+import numpy as np
+
+import oracle as O
+
+
+def _np(t):
+    return t.numpy().view(np.uint64)
+
+
+class CpuShardOps:
+    def prepare(self, log_n):
+        pass
+
+    def synthetic(self, out, log_n, first_col):
+        _np(out)[:] = O.synthetic_trace(out.shape[0], log_n, col_offset=first_col)
+
+    def coeffs(self, trace, out, log_n):
+        # n * monomials in bit-reversed order
+        n = 1 << log_n
+        for c in range(trace.shape[0]):
+            mono = O.ifft_natural_to_natural(_np(trace)[c])
+            br = O.bitreverse(mono).astype(object)
+            _np(out)[c] = np.array([(int(v) * n) % O.P for v in br], dtype=np.uint64)
+
+    def lde_shard(self, coeffs, log_n, log_lde, log_shards, shard, work, lde):
+        n = 1 << log_n
+        n_inv = O.gl_inv(n)
+        m = (n << log_lde) >> log_shards
+        cosets = O.lde_cosets(log_n, log_lde)
+        for c in range(coeffs.shape[0]):
+            mono = O.bitreverse(_np(coeffs)[c])
+            mono = np.array([O.gl_mul(int(v), n_inv) for v in mono], dtype=np.uint64)
+            flat = np.concatenate([O.fft_natural_to_bitreversed(mono, int(s)) for s in cosets])
+            _np(lde)[c] = flat[shard * m:(shard + 1) * m]
+
+    def leaves(self, lde, out):
+        src = _np(lde)
+        _np(out)[:] = np.stack([O.hash_into_leaf(np.ascontiguousarray(src[:, r])) for r in range(src.shape[1])])
+
+    def nodes(self, leaves, cap_size, out):
+        lv = _np(leaves)
+        # merkle_construct hashes leaves from elements; rebuild the node levels directly
+        cur = lv.copy()
+        res = []
+        while cur.shape[0] > cap_size:
+            nxt = np.stack([O.hash_into_node(cur[2 * i], cur[2 * i + 1]) for i in range(cur.shape[0] // 2)])
+            res.append(nxt)
+            cur = nxt
+        _np(out)[:] = np.concatenate(res)

@@ -1,0 +1,37 @@
+"""One rank of a multi-process sharded commit (spawned by test_sharded_*.py).
+
+Writes rank<P>.npz with its lde slice, leaves, nodes and cap into `outdir`."""
+import os
+import sys
+
+
+def run(rank, world, port, cfg, outdir, device, paths):
+    for p in paths:
+        if p not in sys.path:
+            sys.path.insert(0, p)
+    import numpy as np
+    import torch
+    import torch.distributed as dist
+
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        from boojum_amd.sharded import ShardedWorkspace, sharded_witness_commit
+        n_cols, log_n, log_lde, cap = cfg
+        if device == "cpu":
+            from shard_cpu_ops import CpuShardOps
+            ops, dev = CpuShardOps(), "cpu"
+        else:
+            torch.cuda.set_device(0)
+            ops, dev = None, "cuda:0"
+        ws = ShardedWorkspace(n_cols, log_n, log_lde, cap, rank, world, device=dev, ops=ops)
+        tr = ws.synthetic_trace_shard()
+        sharded_witness_commit(tr, ws)
+        if dev != "cpu":
+            torch.cuda.synchronize()
+        u = lambda t: t.cpu().numpy().view(np.uint64)  # noqa: E731
+        np.savez(os.path.join(outdir, "rank%d.npz" % rank), lde=u(ws.lde), leaves=u(ws.leaves), nodes=u(ws.nodes),
+                 cap=u(ws.cap))
+    finally:
+        dist.destroy_process_group()

@@ -1,0 +1,51 @@
+"""Launch a G-rank sharded commit (gloo) and check every rank's outputs against the oracle's
+single-process commit of the same synthetic trace.  Shared by the CPU and GPU tests."""
+import os
+import socket
+
+import numpy as np
+
+import oracle as O
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+ROOT = os.path.dirname(HERE)
+PATHS = [HERE, ROOT, os.path.join(ROOT, "era-boojum_amd"), os.path.join(ROOT, "oracle")]
+
+
+def free_port():
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+def run_and_check(world, cfg, tmp_path, device):
+    import torch.multiprocessing as mp
+    import shard_worker
+    mp.start_processes(shard_worker.run, args=(world, free_port(), cfg, str(tmp_path), device, PATHS), nprocs=world,
+                       join=True, start_method="spawn")
+    n_cols, log_n, log_lde, cap = cfg
+    n, nl = 1 << log_n, 1 << (log_n + log_lde)
+    m = nl // world
+    ref = O.lde_commit(O.synthetic_trace(n_cols, log_n), log_lde, cap, threads=4)
+    lde_flat = ref["lde"].reshape(n_cols, nl)
+    # global node levels: level k (k >= 1) holds nl >> k digests
+    offs, o = [], 0
+    k = 1
+    while (nl >> k) >= cap:
+        offs.append(o)
+        o += nl >> k
+        k += 1
+    for P in range(world):
+        r = np.load(os.path.join(str(tmp_path), "rank%d.npz" % P))
+        assert np.array_equal(r["lde"], lde_flat[:, P * m:(P + 1) * m]), "rank %d lde" % P
+        assert np.array_equal(r["leaves"], ref["leaves"][P * m:(P + 1) * m]), "rank %d leaves" % P
+        assert np.array_equal(r["cap"], ref["cap"]), "rank %d cap" % P
+        # local subtree level k == slice of global level k
+        lo, k = 0, 1
+        while (m >> k) >= max(1, cap // world):
+            cnt = m >> k
+            want = ref["nodes"][offs[k - 1] + P * cnt: offs[k - 1] + (P + 1) * cnt]
+            assert np.array_equal(r["nodes"][lo:lo + cnt], want), "rank %d node level %d" % (P, k)
+            lo += cnt
+            k += 1
+        assert lo == r["nodes"].shape[0]

@@ -1,0 +1,60 @@
+"""GPU parity of the coset-sharded LDE (bj_lde_coeffs_d / bj_lde_shard_d) and of the
+multi-rank sharded commit on one card (gloo staging; RCCL needs one GPU per rank).
+
+Each shard's LDE must equal the matching leaf range of the oracle's full LDE, bit for bit,
+for G <= D (whole cosets), G > D (folded sub-cosets, F = G/D up to 8) and sizes on both the
+generic and the register-resident (n >= 2^18) NTT paths."""
+import numpy as np
+import pytest
+
+import oracle as O
+
+pytestmark = pytest.mark.gpu
+
+
+@pytest.fixture(scope="module")
+def torch_mod():
+    import torch
+    assert torch.cuda.is_available(), "gpu tests need a GPU"
+    import boojum_amd
+    boojum_amd.load()
+    return torch
+
+
+@pytest.mark.parametrize("c,log_n,log_d,log_g", [
+    (3, 6, 1, 1), (3, 6, 1, 2), (2, 8, 2, 1), (2, 8, 2, 3), (5, 10, 1, 4), (2, 12, 3, 3), (2, 12, 1, 3),
+    (1, 19, 1, 2), (1, 19, 2, 3), (1, 18, 1, 1)])
+def test_lde_shard_matches_full_lde(torch_mod, c, log_n, log_d, log_g):
+    torch = torch_mod
+    from boojum_amd._lib import call
+    from boojum_amd.field import stream_of, to_device, to_host
+    n, nl = 1 << log_n, 1 << (log_n + log_d)
+    m = nl >> log_g
+    x = np.random.default_rng(c * 1000 + log_n * 10 + log_g).integers(0, O.P, size=(c, n), dtype=np.uint64)
+    _, ref = O.lde(x, log_d, threads=8)
+    ref = ref.reshape(c, nl)
+    tr = to_device(x)
+    co = torch.empty((c, n), dtype=torch.int64, device="cuda")
+    call("bj_lde_coeffs_d", tr.data_ptr(), c, n, log_n, co.data_ptr(), n, stream_of(co))
+    work = torch.empty((c, m), dtype=torch.int64, device="cuda")
+    for P in range(1 << log_g):
+        lde = torch.empty((c, m), dtype=torch.int64, device="cuda")
+        call("bj_lde_shard_d", co.data_ptr(), c, n, log_n, log_d, log_g, P, work.data_ptr(), lde.data_ptr(),
+             stream_of(lde))
+        got = to_host(lde)
+        assert np.array_equal(got, ref[:, P * m:(P + 1) * m]), "shard %d of %d" % (P, 1 << log_g)
+
+
+def test_lde_shard_errors(torch_mod):
+    from boojum_amd import BoojumError
+    from boojum_amd._lib import call
+    with pytest.raises(BoojumError):
+        call("bj_lde_shard_d", None, 1, 16, 4, 1, 2, 4, None, None, None)   # shard >= G
+    with pytest.raises(BoojumError):
+        call("bj_lde_shard_d", None, 1, 16, 4, 1, 2, 1, None, None, None)   # G > D without work
+
+
+@pytest.mark.parametrize("world,cfg", [(2, (8, 10, 1, 16)), (4, (8, 9, 1, 2))])
+def test_sharded_commit_multirank_one_gpu(torch_mod, world, cfg, tmp_path):
+    from sharded_check import run_and_check
+    run_and_check(world, cfg, tmp_path, "cuda")

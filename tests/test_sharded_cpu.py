@@ -1,0 +1,29 @@
+"""Multi-process (gloo, CPU) tests of the coset-sharded commit orchestration
+(boojum_amd/sharded.py) with the oracle standing in for the HIP steps: column-shard
+ownership, the coefficient all-gather order, leaf-range ownership for G <= D (whole
+cosets) and G > D (sub-cosets), subtree nodes as slices of the reference tree, and cap
+assembly for cap >= G and cap < G (top levels hashed redundantly)."""
+import pytest
+
+from sharded_check import run_and_check
+
+
+@pytest.mark.parametrize("world,cfg", [
+    (2, (4, 5, 1, 4)),    # G == D, cap >= G
+    (2, (2, 4, 2, 2)),    # G < D
+    (4, (4, 4, 1, 2)),    # G > D (sub-cosets), cap < G
+    (4, (8, 5, 2, 16)),   # G == D, cap > G
+])
+def test_sharded_commit_gloo(world, cfg, tmp_path):
+    run_and_check(world, cfg, tmp_path, "cpu")
+
+
+def test_workspace_rejects_bad_shapes():
+    from boojum_amd.sharded import ShardedWorkspace
+    from shard_cpu_ops import CpuShardOps
+    with pytest.raises(ValueError):
+        ShardedWorkspace(3, 4, 1, 2, 0, 2, device="cpu", ops=CpuShardOps())   # C % G
+    with pytest.raises(ValueError):
+        ShardedWorkspace(4, 4, 1, 2, 0, 3, device="cpu", ops=CpuShardOps())   # G not 2^k
+    with pytest.raises(ValueError):
+        ShardedWorkspace(4, 1, 1, 2, 0, 8, device="cpu", ops=CpuShardOps())   # G > leaves
