@@ -5,7 +5,7 @@ pool); this is its multi-GPU split (BASELINE north_star):
 
   * the trace is column-sharded: rank P holds columns [P*C/G, (P+1)*C/G);
   * each rank inverse-transforms its own columns into the exchange format
-    (bj_lde_coeffs_d: n * monomials in bit-reversed order), straight into its slice of
+    (bj_lde_coeffs_d: monomials in bit-reversed order), straight into its slice of
     the all-columns coefficient buffer;
   * one all-gather (RCCL, in place) gives every rank every column's coefficients
     (8 n C bytes in total) -- the only data-path exchange;

@@ -53,3 +53,14 @@ hipError_t launch_lde_forward_fast(uint64_t* lde, size_t lde_col_stride, uint32_
                                    size_t raw_stride, bool raw_bitrev, uint32_t n_cols, uint32_t log_n,
                                    const uint64_t* tw_pyr, const uint64_t* pw, size_t pw_stride, hipStream_t st);
 }  // namespace bj
+
+namespace bj {
+// ntt_ct.hip: coset-folded Cooley-Tukey passes for 2^18 <= n <= 2^23
+bool ct_ntt_supported(uint32_t log_n);
+hipError_t launch_ct_table(uint64_t* out, uint32_t log_n, bool inverse, uint64_t shift, uint64_t scale1,
+                           hipStream_t st);
+hipError_t launch_ct(uint64_t* dst, size_t dst_col_stride, size_t coset_stride, uint32_t n_cosets,
+                     const uint64_t* src, size_t src_stride, bool src_bitrev, uint32_t n_cols, uint32_t log_n,
+                     const uint64_t* tab, size_t tab_stride, uint64_t kappa, bool canon_out, hipStream_t st);
+hipError_t launch_scale(uint64_t* cols, size_t stride, uint32_t n_cols, size_t n, uint64_t k, hipStream_t st);
+}  // namespace bj

@@ -46,6 +46,8 @@ struct Cache {
     std::map<std::tuple<int, uint32_t, int>, uint64_t*> pyr;
     std::map<std::tuple<int, uint32_t, uint64_t, uint64_t>, std::pair<uint64_t*, uint64_t*>> pw;
     std::map<std::tuple<int, uint32_t, uint32_t, int>, uint64_t*> lde_pw;
+    std::map<std::tuple<int, uint32_t, int, uint64_t>, uint64_t*> ct;
+    std::map<std::tuple<int, uint32_t, uint32_t>, uint64_t*> ct_lde;
 };
 Cache& cache() {
     static Cache* c = new Cache();
@@ -153,6 +155,57 @@ int get_lde_powers(uint32_t log_n, uint32_t log_d, bool with_ninv, const uint64_
     return BJ_OK;
 }
 
+// Coset-folded CT twiddle table (ntt_ct.hip) for shift s, n entries. The inverse table
+// (s = 1) carries n^-1 in its stage-0 entry.
+int get_ct(uint32_t log_n, bool inverse, uint64_t shift_, const uint64_t** out) {
+    int dev = 0;
+    HIP_TRY(hipGetDevice(&dev), "hipGetDevice");
+    const uint64_t shift = gl::canon(shift_);
+    Cache& c = cache();
+    std::lock_guard<std::mutex> lk(c.mu);
+    auto key = std::make_tuple(dev, log_n, inverse ? 1 : 0, shift);
+    auto it = c.ct.find(key);
+    if (it != c.ct.end()) { *out = it->second; return BJ_OK; }
+    uint64_t* p = nullptr;
+    HIP_TRY(hipMalloc(&p, ((size_t)1 << log_n) * sizeof(uint64_t)), "hipMalloc(ct table)");
+    hipStream_t st;
+    HIP_TRY(hipStreamCreateWithFlags(&st, hipStreamNonBlocking), "hipStreamCreate");
+    const uint64_t scale1 = inverse ? gl::canon(gl::inv((uint64_t)1 << log_n)) : 1;
+    hipError_t e = bj::launch_ct_table(p, log_n, inverse, shift, scale1, st);
+    if (e == hipSuccess) e = hipStreamSynchronize(st);
+    (void)hipStreamDestroy(st);
+    if (e != hipSuccess) { (void)hipFree(p); return hip_fail(e, "ct table"); }
+    c.ct[key] = p;
+    *out = p;
+    return BJ_OK;
+}
+
+// The D coset tables of an LDE, table i (shift 7 * w_{nD}^bitrev(i)) at out + i * n.
+int get_ct_lde(uint32_t log_n, uint32_t log_d, const uint64_t** out) {
+    int dev = 0;
+    HIP_TRY(hipGetDevice(&dev), "hipGetDevice");
+    Cache& c = cache();
+    std::lock_guard<std::mutex> lk(c.mu);
+    auto key = std::make_tuple(dev, log_n, log_d);
+    auto it = c.ct_lde.find(key);
+    if (it != c.ct_lde.end()) { *out = it->second; return BJ_OK; }
+    const size_t n = (size_t)1 << log_n;
+    const uint32_t D = 1u << log_d;
+    uint64_t* p = nullptr;
+    HIP_TRY(hipMalloc(&p, D * n * sizeof(uint64_t)), "hipMalloc(ct lde tables)");
+    hipStream_t st;
+    HIP_TRY(hipStreamCreateWithFlags(&st, hipStreamNonBlocking), "hipStreamCreate");
+    hipError_t e = hipSuccess;
+    for (uint32_t i = 0; i < D && e == hipSuccess; i++)
+        e = bj::launch_ct_table(p + i * n, log_n, false, lde_coset(log_n, log_d, i), 1, st);
+    if (e == hipSuccess) e = hipStreamSynchronize(st);
+    (void)hipStreamDestroy(st);
+    if (e != hipSuccess) { (void)hipFree(p); return hip_fail(e, "ct lde tables"); }
+    c.ct_lde[key] = p;
+    *out = p;
+    return BJ_OK;
+}
+
 inline bool is_pow2(size_t x) { return x && !(x & (x - 1)); }
 
 int log2_exact(size_t len, uint32_t* out) {
@@ -182,6 +235,57 @@ struct DBuf {
 
 }  // namespace
 
+namespace {
+// Inverse transform of the trace into monomials c_j stored at bitrev_n(j) (the exchange
+// format of bj_lde_coeffs_d), canonical.
+int inverse_to_bitrev(uint64_t* dst, size_t dst_stride, const uint64_t* src, size_t src_stride, uint32_t n_cols,
+                      uint32_t log_n, hipStream_t st) {
+    if (bj::ct_ntt_supported(log_n)) {
+        const uint64_t* tab;
+        if (int r = get_ct(log_n, true, 1, &tab)) return r;
+        HIP_TRY(bj::launch_ct(dst, dst_stride, 0, 1, src, src_stride, false, n_cols, log_n, tab, 0,
+                              gl::canon(gl::inv((uint64_t)1 << log_n)), true, st),
+                "ifft");
+        return BJ_OK;
+    }
+    const uint64_t* ipyr;
+    if (int r = get_pyramid(log_n, true, &ipyr)) return r;
+    HIP_TRY(bj::launch_dif(dst, dst_stride, src, src_stride, n_cols, log_n, ipyr, false, st), "ifft");
+    if (log_n)
+        HIP_TRY(bj::launch_scale(dst, dst_stride, n_cols, (size_t)1 << log_n, gl::canon(gl::inv((uint64_t)1 << log_n)),
+                                 st),
+                "scale");
+    else
+        HIP_TRY(bj::launch_scale(dst, dst_stride, n_cols, 1, 1, st), "canon");
+    return BJ_OK;
+}
+
+// Forward coset transforms of bit-reversed monomials (or natural ones, src_bitrev false) for
+// the n_cosets cosets [first, first + n_cosets) of a 2^log_lde LDE.
+int lde_forward(uint64_t* lde, size_t col_stride, size_t coset_stride, uint32_t first, uint32_t n_cosets,
+                const uint64_t* src, size_t src_stride, bool src_bitrev, uint32_t n_cols, uint32_t log_n,
+                uint32_t log_lde, hipStream_t st) {
+    const size_t n = (size_t)1 << log_n;
+    if (bj::ct_ntt_supported(log_n)) {
+        const uint64_t* tabs;
+        if (int r = get_ct_lde(log_n, log_lde, &tabs)) return r;
+        HIP_TRY(bj::launch_ct(lde, col_stride, coset_stride, n_cosets, src, src_stride, src_bitrev, n_cols, log_n,
+                              tabs + (size_t)first * n, n, 0, true, st),
+                "coset fft");
+        return BJ_OK;
+    }
+    const uint64_t *pyr, *pw;
+    size_t pws;
+    if (int r = get_pyramid(log_n, false, &pyr)) return r;
+    if (int r = get_lde_powers(log_n, log_lde, false, &pw, &pws)) return r;
+    if (coset_stride != n) return fail(BJ_EINVAL, "internal: coset stride");
+    HIP_TRY(bj::launch_lde_forward(lde, col_stride, n_cosets, src, src_stride, src_bitrev, n_cols, log_n, pyr,
+                                   pw + (size_t)first * pws, pws, st),
+            "coset fft");
+    return BJ_OK;
+}
+}  // namespace
+
 extern "C" {
 
 const char* bj_last_error(void) { return g_err.c_str(); }
@@ -192,6 +296,8 @@ int bj_prepare(uint32_t log_n) {
     const uint64_t* t;
     if (int r = get_pyramid(log_n, false, &t)) return r;
     if (int r = get_pyramid(log_n, true, &t)) return r;
+    if (bj::ct_ntt_supported(log_n))
+        if (int r = get_ct(log_n, true, 1, &t)) return r;
     return BJ_OK;
 }
 
@@ -220,13 +326,23 @@ int bj_distribute_powers_d(uint64_t* cols, uint32_t n_cols, size_t col_stride, u
     return BJ_OK;
 }
 
-// The device transform is a DIF network over its own cached twiddle pyramid; a twiddle
-// pointer in the reference's format is accepted for signature parity and not read.
+// Large sizes (2^18..2^23) run the coset-folded CT network of ntt_ct.hip, the shift folded
+// into its twiddle table; other sizes a DIF network (ntt_dif.hip) over its own cached twiddle
+// pyramid. A twiddle pointer in the reference's format is accepted for signature parity and
+// not read.
 int bj_fft_natural_to_bitreversed_d(uint64_t* cols, uint32_t n_cols, size_t col_stride, uint32_t log_n,
                                     uint64_t coset, const uint64_t* twiddles_d, void* stream) {
     (void)twiddles_d;
     if (int r = check_log_n(log_n)) return r;
     if (n_cols == 0) return BJ_OK;
+    if (bj::ct_ntt_supported(log_n)) {
+        const uint64_t* tab;
+        if (int r = get_ct(log_n, false, coset, &tab)) return r;
+        HIP_TRY(bj::launch_ct(cols, col_stride, 0, 1, cols, col_stride, false, n_cols, log_n, tab, 0, 0, true,
+                              S(stream)),
+                "fft");
+        return BJ_OK;
+    }
     if (gl::canon(coset) != 1)
         if (int r = bj_distribute_powers_d(cols, n_cols, col_stride, log_n, coset, stream)) return r;
     const uint64_t* pyr;
@@ -235,26 +351,26 @@ int bj_fft_natural_to_bitreversed_d(uint64_t* cols, uint32_t n_cols, size_t col_
     return BJ_OK;
 }
 
+
 int bj_ifft_natural_to_natural_d(uint64_t* cols, uint32_t n_cols, size_t col_stride, uint32_t log_n,
                                  uint64_t coset, const uint64_t* inv_twiddles_d, void* stream) {
     (void)inv_twiddles_d;
     if (int r = check_log_n(log_n)) return r;
     if (n_cols == 0) return BJ_OK;
     const size_t n = (size_t)1 << log_n;
-    const uint64_t* pyr;
-    if (int r = get_pyramid(log_n, true, &pyr)) return r;
-    // inverse DIF (bit-reversed out) into a temporary, then bit-reverse * n^-1 back in place
+    // monomials in bit-reversed order into a temporary, then the bit reversal back in place
     uint64_t* tmp = nullptr;
     HIP_TRY(hipMallocAsync((void**)&tmp, n * n_cols * 8, S(stream)), "hipMallocAsync");
-    hipError_t e = bj::launch_dif(tmp, n, cols, col_stride, n_cols, log_n, pyr, false, S(stream));
-    const uint64_t n_inv = log_n ? gl::canon(gl::inv((uint64_t)n)) : 1;
-    if (e == hipSuccess) e = bj::launch_bitrev_scale(cols, col_stride, tmp, n, n_cols, log_n, n_inv, S(stream));
+    int r = inverse_to_bitrev(tmp, n, cols, col_stride, n_cols, log_n, S(stream));
+    hipError_t e = r == BJ_OK ? bj::launch_bitrev_scale(cols, col_stride, tmp, n, n_cols, log_n, 1, S(stream))
+                              : hipSuccess;
     hipError_t e2 = hipFreeAsync(tmp, S(stream));
-    if (e != hipSuccess) return hip_fail(e, "ifft");
+    if (r) return r;
+    if (e != hipSuccess) return hip_fail(e, "ifft bitreverse");
     if (e2 != hipSuccess) return hip_fail(e2, "hipFreeAsync");
     if (gl::canon(coset) != 1) {
         const uint64_t *lo, *hi;
-        if (int r = get_powers(log_n, gl::inv(gl::canon(coset)), 1, &lo, &hi)) return r;
+        if (int r2 = get_powers(log_n, gl::inv(gl::canon(coset)), 1, &lo, &hi)) return r2;
         HIP_TRY(bj::launch_distribute(cols, col_stride, n_cols, log_n, lo, hi, S(stream)), "distribute");
     }
     return BJ_OK;
@@ -267,14 +383,7 @@ int bj_monomials_to_lde_d(const uint64_t* monomials, uint32_t n_cols, size_t mon
     if (n_cols == 0) return BJ_OK;
     const size_t n = (size_t)1 << log_n;
     const uint32_t D = 1u << log_lde;
-    const uint64_t *pyr, *pw;
-    size_t pws;
-    if (int r = get_pyramid(log_n, false, &pyr)) return r;
-    if (int r = get_lde_powers(log_n, log_lde, false, &pw, &pws)) return r;
-    HIP_TRY(bj::launch_lde_forward(lde, (size_t)D * n, D, monomials, mono_stride, false, n_cols, log_n, pyr, pw, pws,
-                                   S(stream)),
-            "coset fft");
-    return BJ_OK;
+    return lde_forward(lde, (size_t)D * n, n, 0, D, monomials, mono_stride, false, n_cols, log_n, log_lde, S(stream));
 }
 
 int bj_lde_d(const uint64_t* trace, uint32_t n_cols, size_t trace_stride, uint32_t log_n, uint32_t log_lde,
@@ -284,28 +393,17 @@ int bj_lde_d(const uint64_t* trace, uint32_t n_cols, size_t trace_stride, uint32
     if (n_cols == 0) return BJ_OK;
     const size_t n = (size_t)1 << log_n;
     const uint32_t D = 1u << log_lde;
-    const uint64_t *ipyr, *pyr, *pw;
-    size_t pws;
-    if (int r = get_pyramid(log_n, true, &ipyr)) return r;
-    if (int r = get_pyramid(log_n, false, &pyr)) return r;
-    if (int r = get_lde_powers(log_n, log_lde, true, &pw, &pws)) return r;
-    // iFFT (utils.rs:295-304) as an inverse DIF: scratch = n * monomials in bit-reversed
-    // order; the forward pass gathers it back in natural order and folds n^-1 into the
-    // coset powers (utils.rs:363-379), all D cosets per tile load.
-    HIP_TRY(bj::launch_dif(scratch, n, trace, trace_stride, n_cols, log_n, ipyr, false, S(stream)), "ifft");
-    HIP_TRY(bj::launch_lde_forward(lde, (size_t)D * n, D, scratch, n, true, n_cols, log_n, pyr, pw, pws, S(stream)),
-            "coset fft");
-    return BJ_OK;
+    // iFFT (utils.rs:295-304): scratch = monomials in bit-reversed order; the forward pass
+    // gathers them back in natural order, all D cosets (utils.rs:363-379).
+    if (int r = inverse_to_bitrev(scratch, n, trace, trace_stride, n_cols, log_n, S(stream))) return r;
+    return lde_forward(lde, (size_t)D * n, n, 0, D, scratch, n, true, n_cols, log_n, log_lde, S(stream));
 }
 
 int bj_lde_coeffs_d(const uint64_t* trace, uint32_t n_cols, size_t trace_stride, uint32_t log_n, uint64_t* coeffs,
                     size_t coeffs_stride, void* stream) {
     if (int r = check_log_n(log_n)) return r;
     if (n_cols == 0) return BJ_OK;
-    const uint64_t* ipyr;
-    if (int r = get_pyramid(log_n, true, &ipyr)) return r;
-    HIP_TRY(bj::launch_dif(coeffs, coeffs_stride, trace, trace_stride, n_cols, log_n, ipyr, false, S(stream)), "ifft");
-    return BJ_OK;
+    return inverse_to_bitrev(coeffs, coeffs_stride, trace, trace_stride, n_cols, log_n, S(stream));
 }
 
 int bj_lde_shard_d(const uint64_t* coeffs, uint32_t n_cols, size_t coeffs_stride, uint32_t log_n, uint32_t log_lde,
@@ -316,32 +414,31 @@ int bj_lde_shard_d(const uint64_t* coeffs, uint32_t n_cols, size_t coeffs_stride
     if (shard >= (1u << log_shards)) return fail(BJ_EINVAL, "shard index out of range");
     if (n_cols == 0) return BJ_OK;
     const size_t n = (size_t)1 << log_n;
-    const uint64_t* pyr;
     if (log_shards <= log_lde) {
         // whole cosets [P * D/G, (P+1) * D/G)
         const uint32_t per = 1u << (log_lde - log_shards);
-        const uint64_t* pw;
-        size_t pws;
-        if (int r = get_pyramid(log_n, false, &pyr)) return r;
-        if (int r = get_lde_powers(log_n, log_lde, true, &pw, &pws)) return r;
-        HIP_TRY(bj::launch_lde_forward(lde, (size_t)per * n, per, coeffs, coeffs_stride, true, n_cols, log_n, pyr,
-                                       pw + (size_t)shard * per * pws, pws, S(stream)),
-                "coset fft");
-        return BJ_OK;
+        return lde_forward(lde, (size_t)per * n, n, shard * per, per, coeffs, coeffs_stride, true, n_cols, log_n,
+                           log_lde, S(stream));
     }
     const uint32_t log_f = log_shards - log_lde;
     if ((1u << log_f) > bj::kMaxFold) return fail(BJ_EINVAL, "G / D exceeds 64");
     if (!work) return fail(BJ_EINVAL, "work buffer required when shards exceed the lde degree");
     const uint32_t log_m = log_n - log_f;
     const size_t m = (size_t)1 << log_m;
-    // s' = 7 * w_{nD}^{bitrev_{log G}(P)}; h_t = sum_a c_{t+am} (s'^m)^a (shard.hip)
+    // s' = 7 * w_{nD}^{bitrev_{log G}(P)}; h_t = sum_a c_{t+am} (s'^m)^a (shard.hip), then the
+    // m-point coset-s' transform of h
     const uint64_t g = gl::domain_generator(log_n + log_lde);
     const uint64_t sp = gl::canon(gl::mul(gl::pow(g, gl::bitrev32(shard, log_shards)), gl::GENERATOR));
-    const uint64_t *lo, *hi;
-    const uint64_t scale = gl::canon(gl::inv((uint64_t)n));  // coeffs hold n * c_j
-    if (int r = get_pyramid(log_m, false, &pyr)) return r;
-    if (int r = get_powers(log_m, sp, scale, &lo, &hi)) return r;
     HIP_TRY(bj::launch_fold(work, m, coeffs, coeffs_stride, n_cols, log_m, log_f, gl::pow(sp, m), S(stream)), "fold");
+    if (bj::ct_ntt_supported(log_m)) {
+        const uint64_t* tab;
+        if (int r = get_ct(log_m, false, sp, &tab)) return r;
+        HIP_TRY(bj::launch_ct(lde, m, 0, 1, work, m, true, n_cols, log_m, tab, 0, 0, true, S(stream)), "coset fft");
+        return BJ_OK;
+    }
+    const uint64_t *pyr, *lo, *hi;
+    if (int r = get_pyramid(log_m, false, &pyr)) return r;
+    if (int r = get_powers(log_m, sp, 1, &lo, &hi)) return r;
     HIP_TRY(bj::launch_lde_forward(lde, m, 1, work, m, true, n_cols, log_m, pyr, lo, 4096 + bj::pw_hi_len(log_m),
                                    S(stream)),
             "coset fft");

@@ -1,0 +1,402 @@
+// Coset-folded Cooley-Tukey NTT passes for the large sizes (2^18 <= n <= 2^23).
+//
+// The reference's transform is serial_ct_ntt_natural_to_bitreversed (fft/mod.rs:659-734):
+// at the stage with 2^u groups, group k pairs (j, j + h) and does
+//   (a, c) <- (a + mu_k c, a - mu_k c),   mu_k = omegas_bit_reversed[k] = w_{2^(u+1)}^bitrev_u(k).
+// The coset FFT (fft/mod.rs:398-411) first multiplies x_j by s^j (distribute_powers,
+// :308-317). That shift folds into the butterflies. After stage u, group k evaluates its
+// half-size polynomial on the coset sigma_k <w_m> with sigma_k = s * w_n^bitrev_u(k). So the
+// shifted transform is the same network with
+//   mu_k(s) = s^(n >> (u+1)) * w_{2^(u+1)}^bitrev_u(k)
+// and no per-element powers at all. Same field values, so outputs (canonicalised) are
+// bit-identical to the reference's.
+//
+// Twiddle table per shift: CT[2^u + k] = mu_k(s), for u < log n, k < 2^u (n entries, CT[0]
+// unused). The inverse table (w^-1, s = 1) carries n^-1 in CT[1], and the head kernel
+// multiplies the stage-0 lower operands by n^-1 as well, so the inverse transform returns
+// the monomials themselves (utils.rs:295-304 after ifft's x n^-1), not n * monomials.
+//
+// Tiling is that of ntt_fast.hip. Each thread holds 32 elements in VGPRs and runs up to five
+// stages in registers; LDS (XOR-swizzled) only re-deals elements between register phases.
+// * head: the first R = log n - 13 stages on tiles of 2^R rows x 2^(13-R) adjacent columns.
+//   Stage v's group index is the row's top v bits, so in phase A' the twiddles are
+//   wave-uniform (scalar loads) and in phase B' a per-thread base + constant.
+// * tail: the last 13 stages on contiguous 8192-element blocks, with the group index
+//   (q << v) + (offset >> (13 - v)) for tile q. A tile reads its own 8191-entry slice of the
+//   table, and all columns (blockIdx.x) of one tile share that slice in L2.
+// MODE 1 heads gather a bit-reversed source (the iNTT output, c_j at bitrev_n(j)) in runs of
+// 2^R words, so the iFFT's bit reversal (fft/mod.rs:481) never costs a pass of its own.
+#include <hip/hip_runtime.h>
+#include "gl.hpp"
+#include "gl_asm.hpp"
+#include "bj_internal.hpp"
+
+namespace bj {
+
+namespace {
+
+constexpr int NT = 256;
+constexpr int PT = 32;
+constexpr int TILE = NT * PT;
+
+__device__ __forceinline__ void split2(uint64_t x, uint32_t& lo, uint32_t& hi) {
+    lo = (uint32_t)x;
+    hi = (uint32_t)(x >> 32);
+}
+__device__ __forceinline__ uint64_t join2(uint32_t lo, uint32_t hi) { return ((uint64_t)hi << 32) | lo; }
+
+// CT butterflies on four pairs: t = c * mu; (a, c) <- (a + t, a - t).
+__device__ __forceinline__ void ct_bfly_x4(uint64_t& xa0, uint64_t& xc0, uint64_t& xa1, uint64_t& xc1,
+                                           uint64_t& xa2, uint64_t& xc2, uint64_t& xa3, uint64_t& xc3, uint64_t w0,
+                                           uint64_t w1, uint64_t w2, uint64_t w3) {
+    uint32_t c0[4], c1[4], v0[4], v1[4], t0[4], t1[4];
+    split2(xc0, c0[0], c1[0]); split2(w0, v0[0], v1[0]);
+    split2(xc1, c0[1], c1[1]); split2(w1, v0[1], v1[1]);
+    split2(xc2, c0[2], c1[2]); split2(w2, v0[2], v1[2]);
+    split2(xc3, c0[3], c1[3]); split2(w3, v0[3], v1[3]);
+    glasm::mul_x4(c0[0], c1[0], v0[0], v1[0], t0[0], t1[0], c0[1], c1[1], v0[1], v1[1], t0[1], t1[1],
+                  c0[2], c1[2], v0[2], v1[2], t0[2], t1[2], c0[3], c1[3], v0[3], v1[3], t0[3], t1[3]);
+    uint32_t a0[4], a1[4], s0[4], s1[4], d0[4], d1[4];
+    split2(xa0, a0[0], a1[0]); split2(xa1, a0[1], a1[1]);
+    split2(xa2, a0[2], a1[2]); split2(xa3, a0[3], a1[3]);
+    glasm::add_x4(a0[0], a1[0], t0[0], t1[0], s0[0], s1[0], a0[1], a1[1], t0[1], t1[1], s0[1], s1[1],
+                  a0[2], a1[2], t0[2], t1[2], s0[2], s1[2], a0[3], a1[3], t0[3], t1[3], s0[3], s1[3]);
+    glasm::sub_x4(a0[0], a1[0], t0[0], t1[0], d0[0], d1[0], a0[1], a1[1], t0[1], t1[1], d0[1], d1[1],
+                  a0[2], a1[2], t0[2], t1[2], d0[2], d1[2], a0[3], a1[3], t0[3], t1[3], d0[3], d1[3]);
+    xa0 = join2(s0[0], s1[0]); xc0 = join2(d0[0], d1[0]);
+    xa1 = join2(s0[1], s1[1]); xc1 = join2(d0[1], d1[1]);
+    xa2 = join2(s0[2], s1[2]); xc2 = join2(d0[2], d1[2]);
+    xa3 = join2(s0[3], s1[3]); xc3 = join2(d0[3], d1[3]);
+}
+
+__device__ __forceinline__ void mul4_by(uint64_t& x0, uint64_t& x1, uint64_t& x2, uint64_t& x3, uint64_t k) {
+    uint32_t a0[4], a1[4], z0[4], z1[4], k0, k1;
+    split2(k, k0, k1);
+    split2(x0, a0[0], a1[0]); split2(x1, a0[1], a1[1]);
+    split2(x2, a0[2], a1[2]); split2(x3, a0[3], a1[3]);
+    glasm::mul_x4(a0[0], a1[0], k0, k1, z0[0], z1[0], a0[1], a1[1], k0, k1, z0[1], z1[1],
+                  a0[2], a1[2], k0, k1, z0[2], z1[2], a0[3], a1[3], k0, k1, z0[3], z1[3]);
+    x0 = join2(z0[0], z1[0]); x1 = join2(z0[1], z1[1]);
+    x2 = join2(z0[2], z1[2]); x3 = join2(z0[3], z1[3]);
+}
+
+__device__ __forceinline__ constexpr int pair_lo(int q, int hk) { return (q / hk) * 2 * hk + (q % hk); }
+
+// One register stage on x[32], pairs (k, k + HK); w[q] = twiddle of pair q.
+template <int HK>
+__device__ __forceinline__ void ct_stage(uint64_t* x, const uint64_t* w) {
+#pragma unroll
+    for (int b = 0; b < 4; b++) {
+        const int q0 = 4 * b;
+        ct_bfly_x4(x[pair_lo(q0, HK)], x[pair_lo(q0, HK) + HK], x[pair_lo(q0 + 1, HK)], x[pair_lo(q0 + 1, HK) + HK],
+                   x[pair_lo(q0 + 2, HK)], x[pair_lo(q0 + 2, HK) + HK], x[pair_lo(q0 + 3, HK)],
+                   x[pair_lo(q0 + 3, HK) + HK], w[q0], w[q0 + 1], w[q0 + 2], w[q0 + 3]);
+    }
+}
+
+__device__ __forceinline__ uint64_t canon_u64(uint64_t v) {
+    uint32_t a0, a1, z0, z1;
+    split2(v, a0, a1);
+    glasm::canon_x1(a0, a1, z0, z1);
+    return join2(z0, z1);
+}
+
+// ------------------------------------------------------------------- head
+
+template <int LOGW>
+__device__ __forceinline__ uint32_t swz_head(uint32_t e) {
+    constexpr uint32_t m = LOGW >= 5 ? 0u : ((32u >> LOGW) - 1u);
+    return e ^ (((e >> (5 + LOGW)) & m) << LOGW);
+}
+
+// Phase A' twiddles of stage v (register distance 16 >> v): pair q's group is lo(q) >> (5 - v),
+// the same for every thread.
+template <int V>
+__device__ __forceinline__ void tw_ct_headA(uint64_t* w, const uint64_t* __restrict__ ct) {
+    constexpr int HK = 16 >> V;
+#pragma unroll
+    for (int q = 0; q < 16; q++) w[q] = ct[(1 << V) + (pair_lo(q, HK) >> (5 - V))];
+}
+
+// Phase B' twiddles of stage v >= 5 (rows 32 s + k, register distance 2^(R-1-v)):
+// group (32 s + lo(q)) >> (R - v).
+template <int R, int V>
+__device__ __forceinline__ void tw_ct_headB(uint64_t* w, const uint64_t* __restrict__ ct, uint32_t s) {
+    constexpr int HK = 1 << (R - 1 - V);
+    const uint64_t* base = ct + (1u << V) + ((32u * s) >> (R - V));
+#pragma unroll
+    for (int q = 0; q < 16; q++) w[q] = base[pair_lo(q, HK) >> (R - V)];
+}
+
+template <int R, int V>
+__device__ __forceinline__ void head_b_stage(uint64_t* x, const uint64_t* __restrict__ ct, uint32_t s) {
+    if constexpr (V < R) {
+        uint64_t w[16];
+        tw_ct_headB<R, V>(w, ct, s);
+        ct_stage<(1 << (R - 1 - V))>(x, w);
+        head_b_stage<R, V + 1>(x, ct, s);
+    }
+}
+
+// MODE 0: natural source; MODE 1: bit-reversed source gathered in runs of 2^R words.
+// KAPPA: multiply the stage-0 lower operands by kappa (the inverse table's CT[1] already
+// carries it for the upper ones), i.e. scale the whole transform by kappa.
+template <int R, int MODE, bool KAPPA>
+__global__ __launch_bounds__(NT, 2) void ct_head_kernel(uint64_t* dst, size_t dst_col_stride, size_t coset_stride,
+                                                        const uint64_t* src, size_t src_stride, uint32_t log_n,
+                                                        const uint64_t* __restrict__ tab, size_t tab_stride,
+                                                        uint64_t kappa) {
+    constexpr int LOGW = 13 - R;
+    constexpr uint32_t W = 1u << LOGW;
+    constexpr uint32_t T = 1u << (R - 5);
+    __shared__ uint64_t lds[TILE];
+    const uint32_t tid = threadIdx.x;
+    const size_t n = (size_t)1 << log_n;
+    const size_t S = n >> R;
+    const size_t o0 = (size_t)blockIdx.y * W;
+    const uint64_t* sc = src + (size_t)blockIdx.x * src_stride;
+    const uint64_t* ct = tab + (size_t)blockIdx.z * tab_stride;
+    const uint32_t w = tid & (W - 1);
+    const uint32_t s = tid >> LOGW;
+    const size_t o = o0 + w;
+    uint64_t x[PT];
+    if constexpr (MODE == 0) {
+#pragma unroll
+        for (int k = 0; k < PT; k++) x[k] = sc[(size_t)(s + T * k) * S + o];
+    } else {
+        const uint32_t wg = tid / T, sg = tid % T;
+        const size_t run = (size_t)gl::bitrev32((uint32_t)(o0 + wg), log_n - R) << R;
+#pragma unroll
+        for (int k = 0; k < PT; k++) x[k] = sc[run + sg + T * k];
+#pragma unroll
+        for (int k = 0; k < PT; k++) lds[swz_head<LOGW>(gl::bitrev32(sg + T * k, R) * W + wg)] = x[k];
+        __syncthreads();
+#pragma unroll
+        for (int k = 0; k < PT; k++) x[k] = lds[swz_head<LOGW>((s + T * k) * W + w)];
+    }
+    // phase A': rows s + T k, stages 0..4
+    {
+        uint64_t wa[16], wb[16];
+        tw_ct_headA<0>(wa, ct);
+        tw_ct_headA<1>(wb, ct);
+        if constexpr (KAPPA) {
+#pragma unroll
+            for (int k = 0; k < 16; k += 4) mul4_by(x[k], x[k + 1], x[k + 2], x[k + 3], kappa);
+        }
+        ct_stage<16>(x, wa);
+        tw_ct_headA<2>(wa, ct);
+        ct_stage<8>(x, wb);
+        tw_ct_headA<3>(wb, ct);
+        ct_stage<4>(x, wa);
+        tw_ct_headA<4>(wa, ct);
+        ct_stage<2>(x, wb);
+        ct_stage<1>(x, wa);
+    }
+    if constexpr (MODE == 1) __syncthreads();  // gather reads of lds done
+#pragma unroll
+    for (int k = 0; k < PT; k++) lds[swz_head<LOGW>((s + T * k) * W + w)] = x[k];
+    __syncthreads();
+#pragma unroll
+    for (int k = 0; k < PT; k++) x[k] = lds[swz_head<LOGW>((32 * s + k) * W + w)];
+    head_b_stage<R, 5>(x, ct, s);
+    uint64_t* dc = dst + (size_t)blockIdx.x * dst_col_stride + (size_t)blockIdx.z * coset_stride;
+#pragma unroll
+    for (int k = 0; k < PT; k++) dc[(size_t)(32 * s + k) * S + o] = x[k];
+}
+
+// ------------------------------------------------------------------- tail
+
+__device__ __forceinline__ uint32_t swz_tail(uint32_t e) { return e ^ ((e >> 5) & 31); }
+
+// phase A (element t + 256 k, local stage v = 0..4): group (q << v) + (lo(q) >> (5 - v)),
+// wave-uniform.
+template <int V>
+__device__ __forceinline__ void tw_ct_tailA(uint64_t* w, const uint64_t* __restrict__ ct, uint32_t u0, size_t q) {
+    constexpr int HK = 16 >> V;
+    const uint64_t* base = ct + ((size_t)1 << (u0 + V)) + (q << V);
+#pragma unroll
+    for (int p = 0; p < 16; p++) w[p] = base[pair_lo(p, HK) >> (5 - V)];
+}
+
+// phase B (element (thi << 8) | (k << 3) | tlo, v = 5..9): (q << v) + (thi << (v-5)) + (lo >> (10-v)).
+template <int V>
+__device__ __forceinline__ void tw_ct_tailB(uint64_t* w, const uint64_t* __restrict__ ct, uint32_t u0, size_t q,
+                                            uint32_t thi) {
+    constexpr int HK = 16 >> (V - 5);
+    const uint64_t* base = ct + ((size_t)1 << (u0 + V)) + (q << V) + ((size_t)thi << (V - 5));
+#pragma unroll
+    for (int p = 0; p < 16; p++) w[p] = base[pair_lo(p, HK) >> (10 - V)];
+}
+
+// phase C (element 32 t + k, v = 10..12): (q << v) + (t << (v-8)) + (lo >> (13-v)).
+template <int V>
+__device__ __forceinline__ void tw_ct_tailC(uint64_t* w, const uint64_t* __restrict__ ct, uint32_t u0, size_t q,
+                                            uint32_t t) {
+    constexpr int HK = 4 >> (V - 10);
+    const uint64_t* base = ct + ((size_t)1 << (u0 + V)) + (q << V) + ((size_t)t << (V - 8));
+#pragma unroll
+    for (int p = 0; p < 16; p++) w[p] = base[pair_lo(p, HK) >> (13 - V)];
+}
+
+__global__ __launch_bounds__(NT, 2) void ct_tail_kernel(uint64_t* dst, size_t dst_col_stride, size_t coset_stride,
+                                                        uint32_t log_n, const uint64_t* __restrict__ tab,
+                                                        size_t tab_stride, int canon_out) {
+    __shared__ uint64_t lds[TILE];
+    const uint32_t t = threadIdx.x;
+    const size_t q = blockIdx.y;
+    const uint32_t u0 = log_n - 13;
+    uint64_t* d = dst + (size_t)blockIdx.x * dst_col_stride + (size_t)blockIdx.z * coset_stride + q * TILE;
+    const uint64_t* ct = tab + (size_t)blockIdx.z * tab_stride;
+    uint64_t x[PT], wa[16], wb[16];
+#pragma unroll
+    for (int k = 0; k < PT; k++) x[k] = d[t + NT * k];
+    tw_ct_tailA<0>(wa, ct, u0, q);
+    tw_ct_tailA<1>(wb, ct, u0, q);
+    ct_stage<16>(x, wa);
+    tw_ct_tailA<2>(wa, ct, u0, q);
+    ct_stage<8>(x, wb);
+    tw_ct_tailA<3>(wb, ct, u0, q);
+    ct_stage<4>(x, wa);
+    tw_ct_tailA<4>(wa, ct, u0, q);
+    ct_stage<2>(x, wb);
+    const uint32_t tlo = t & 7, thi = t >> 3;
+    tw_ct_tailB<5>(wb, ct, u0, q, thi);
+    ct_stage<1>(x, wa);
+#pragma unroll
+    for (int k = 0; k < PT; k++) lds[swz_tail(t + NT * k)] = x[k];
+    __syncthreads();
+#pragma unroll
+    for (int k = 0; k < PT; k++) x[k] = lds[swz_tail((thi << 8) | ((uint32_t)k << 3) | tlo)];
+    tw_ct_tailB<6>(wa, ct, u0, q, thi);
+    ct_stage<16>(x, wb);
+    tw_ct_tailB<7>(wb, ct, u0, q, thi);
+    ct_stage<8>(x, wa);
+    tw_ct_tailB<8>(wa, ct, u0, q, thi);
+    ct_stage<4>(x, wb);
+    tw_ct_tailB<9>(wb, ct, u0, q, thi);
+    ct_stage<2>(x, wa);
+    tw_ct_tailC<10>(wa, ct, u0, q, t);
+    ct_stage<1>(x, wb);
+    __syncthreads();
+#pragma unroll
+    for (int k = 0; k < PT; k++) lds[swz_tail((thi << 8) | ((uint32_t)k << 3) | tlo)] = x[k];
+    __syncthreads();
+#pragma unroll
+    for (int k = 0; k < PT; k++) x[k] = lds[swz_tail(t * PT + k)];
+    tw_ct_tailC<11>(wb, ct, u0, q, t);
+    ct_stage<4>(x, wa);
+    tw_ct_tailC<12>(wa, ct, u0, q, t);
+    ct_stage<2>(x, wb);
+    ct_stage<1>(x, wa);
+    __syncthreads();
+#pragma unroll
+    for (int k = 0; k < PT; k++) lds[swz_tail(t * PT + k)] = x[k];
+    __syncthreads();
+#pragma unroll
+    for (int k = 0; k < PT; k++) {
+        const uint64_t v = lds[swz_tail(t + NT * k)];
+        d[t + NT * k] = canon_out ? canon_u64(v) : v;
+    }
+}
+
+// ------------------------------------------------------------ table, scale
+
+struct ShiftPowers {
+    uint64_t sp[33];  // sp[u] = s^(n >> (u + 1))
+};
+
+// CT[2^u + k] = s^(n >> (u+1)) * w_n^(bitrev_u(k) * (n >> (u+1))); CT[1] *= scale1.
+__global__ void ct_table_kernel(uint64_t* out, uint32_t log_n, uint64_t w_n, ShiftPowers spw, uint64_t scale1) {
+    const size_t n = (size_t)1 << log_n;
+    for (size_t i = blockIdx.x * (size_t)blockDim.x + threadIdx.x; i < n; i += (size_t)gridDim.x * blockDim.x) {
+        if (i == 0) {
+            out[0] = 0;
+            continue;
+        }
+        const uint32_t u = 63 - __builtin_clzll(i);
+        const uint32_t k = (uint32_t)(i - ((size_t)1 << u));
+        const uint64_t e = (uint64_t)gl::bitrev32(k, u) << (log_n - u - 1);
+        uint64_t v = gl::mul(gl::pow(w_n, e), spw.sp[u]);
+        if (i == 1) v = gl::mul(v, scale1);
+        out[i] = gl::canon(v);
+    }
+}
+
+__global__ __launch_bounds__(256) void scale_kernel(uint64_t* cols, size_t stride, size_t n, uint64_t k) {
+    uint64_t* c = cols + (size_t)blockIdx.y * stride;
+    for (size_t i = blockIdx.x * (size_t)blockDim.x + threadIdx.x; i < n; i += (size_t)gridDim.x * blockDim.x)
+        c[i] = gl::canon(gl::mul(c[i], k));
+}
+
+template <int R>
+void launch_head_R(int mode, bool kappa_on, dim3 g, uint64_t* dst, size_t dst_col_stride, size_t coset_stride,
+                   const uint64_t* src, size_t src_stride, uint32_t log_n, const uint64_t* tab, size_t tab_stride,
+                   uint64_t kappa, hipStream_t st) {
+#define BJ_CT_HEAD(M, K)                                                                                        \
+    hipLaunchKernelGGL((ct_head_kernel<R, M, K>), g, dim3(NT), 0, st, dst, dst_col_stride, coset_stride, src, \
+                       src_stride, log_n, tab, tab_stride, kappa)
+    if (mode == 0) {
+        if (kappa_on) BJ_CT_HEAD(0, true);
+        else BJ_CT_HEAD(0, false);
+    } else {
+        if (kappa_on) BJ_CT_HEAD(1, true);
+        else BJ_CT_HEAD(1, false);
+    }
+#undef BJ_CT_HEAD
+}
+
+}  // namespace
+
+bool ct_ntt_supported(uint32_t log_n) { return log_n >= 18 && log_n <= 23; }
+
+hipError_t launch_ct_table(uint64_t* out, uint32_t log_n, bool inverse, uint64_t shift, uint64_t scale1,
+                           hipStream_t st) {
+    uint64_t w = gl::domain_generator(log_n);
+    if (inverse) w = gl::canon(gl::inv(w));
+    ShiftPowers spw{};
+    for (uint32_t u = 0; u < log_n; u++) spw.sp[u] = gl::pow(gl::canon(shift), (uint64_t)1 << (log_n - u - 1));
+    const size_t n = (size_t)1 << log_n;
+    size_t blocks = (n + 255) / 256;
+    if (blocks > 8192) blocks = 8192;
+    hipLaunchKernelGGL(ct_table_kernel, dim3((unsigned)blocks), dim3(256), 0, st, out, log_n, w, spw,
+                       gl::canon(scale1));
+    return hipGetLastError();
+}
+
+hipError_t launch_scale(uint64_t* cols, size_t stride, uint32_t n_cols, size_t n, uint64_t k, hipStream_t st) {
+    if (n_cols == 0 || n == 0) return hipSuccess;
+    size_t bx = (n + 255) / 256;
+    if (bx > 4096) bx = 4096;
+    hipLaunchKernelGGL(scale_kernel, dim3((unsigned)bx, n_cols), dim3(256), 0, st, cols, stride, n, k);
+    return hipGetLastError();
+}
+
+// Coset-folded CT transform(s), natural -> bit-reversed, for n_cosets twiddle tables at
+// tab + i * tab_stride. Output (c, i, r) at dst + c * dst_col_stride + i * coset_stride + r.
+// src_bitrev: source holds c_j at bitrev_n(j) (never in place); otherwise natural (in place
+// allowed when dst == src and n_cosets == 1). kappa != 0: scale by kappa (the table's CT[1]
+// must already carry it).
+hipError_t launch_ct(uint64_t* dst, size_t dst_col_stride, size_t coset_stride, uint32_t n_cosets,
+                     const uint64_t* src, size_t src_stride, bool src_bitrev, uint32_t n_cols, uint32_t log_n,
+                     const uint64_t* tab, size_t tab_stride, uint64_t kappa, bool canon_out, hipStream_t st) {
+    if (n_cols == 0 || n_cosets == 0) return hipSuccess;
+    if (!ct_ntt_supported(log_n)) return hipErrorInvalidValue;
+    const size_t n = (size_t)1 << log_n;
+    const unsigned tiles = (unsigned)(n / TILE);
+    const dim3 g(n_cols, tiles, n_cosets);
+    const int mode = src_bitrev ? 1 : 0;
+    const bool k_on = kappa != 0;
+    switch (log_n - 13) {
+        case 5: launch_head_R<5>(mode, k_on, g, dst, dst_col_stride, coset_stride, src, src_stride, log_n, tab, tab_stride, kappa, st); break;
+        case 6: launch_head_R<6>(mode, k_on, g, dst, dst_col_stride, coset_stride, src, src_stride, log_n, tab, tab_stride, kappa, st); break;
+        case 7: launch_head_R<7>(mode, k_on, g, dst, dst_col_stride, coset_stride, src, src_stride, log_n, tab, tab_stride, kappa, st); break;
+        case 8: launch_head_R<8>(mode, k_on, g, dst, dst_col_stride, coset_stride, src, src_stride, log_n, tab, tab_stride, kappa, st); break;
+        case 9: launch_head_R<9>(mode, k_on, g, dst, dst_col_stride, coset_stride, src, src_stride, log_n, tab, tab_stride, kappa, st); break;
+        default: launch_head_R<10>(mode, k_on, g, dst, dst_col_stride, coset_stride, src, src_stride, log_n, tab, tab_stride, kappa, st); break;
+    }
+    hipLaunchKernelGGL(ct_tail_kernel, g, dim3(NT), 0, st, dst, dst_col_stride, coset_stride, log_n, tab, tab_stride,
+                       canon_out ? 1 : 0);
+    return hipGetLastError();
+}
+
+}  // namespace bj

@@ -196,7 +196,7 @@ __global__ __launch_bounds__(DIF_THREADS, 2) void dif_pass_kernel(uint64_t* dst,
 }
 
 // First forward pass of the LDE over all D cosets (u0 = 0).
-// BITREV_SRC: src = raw iNTT output in bit-reversed order (y[r] = n * monomial[bitrev(r)]),
+// BITREV_SRC: src = iNTT output in bit-reversed order (y[r] = monomial[bitrev(r)]),
 //   read with a coalesced gather (tile column w is the contiguous run of 2^R words at
 //   bitrev(o) << R); otherwise src = monomials in natural order (runs of W words).
 // Element j of coset i is src_j * pw_i(j), pw_i(j) = scale * s_i^j from the two-level

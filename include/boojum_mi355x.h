@@ -89,9 +89,8 @@ int bj_ifft_natural_to_natural_h(uint64_t* col, size_t len, uint64_t coset);
  *   monomials[c] = ifft_natural_to_natural(trace[c])
  *   lde[c][i]    = fft_natural_to_bitreversed(monomials[c], 7 * w_{nD}^{bitrev(i)})
  * trace:   n_cols columns of n = 2^log_n at trace + c * trace_stride (read only)
- * scratch: n_cols x n device workspace (on return it holds the raw inverse transform,
- *          n * monomials in bit-reversed order -- an intermediate, like the reference's
- *          consumed monomial vectors; bj_ifft_natural_to_natural_d gives monomials)
+ * scratch: n_cols x n device workspace (on return it holds the monomials in bit-reversed
+ *          order, c_j at bitrev_n(j) -- the format of bj_lde_coeffs_d)
  * lde:     n_cols x D x n, element (c, i, r) at lde + (c * D + i) * n + r
  *          (the reference's per-column Vec<coset> of ArcGenericLdeStorage)
  * D = 2^log_lde. */
@@ -109,8 +108,9 @@ int bj_monomials_to_lde_d(const uint64_t* monomials, uint32_t n_cols, size_t mon
  * into G contiguous ranges of m = n*D/G leaves; rank P owns [P*m, (P+1)*m).
  *
  * Step 1 (every rank, its own trace columns): bj_lde_coeffs_d writes the inverse transform
- *   in the exchange format: column c holds n * c_j at position bitrev_n(j), where c_j are the
- *   monomials of ifft_natural_to_natural (utils.rs:295-304).  Ranks all-gather these columns.
+ *   in the exchange format: column c holds c_j at position bitrev_n(j), where c_j are the
+ *   monomials of ifft_natural_to_natural (utils.rs:295-304), canonical.  Ranks all-gather
+ *   these columns.
  * Step 2 (every rank, all columns): bj_lde_shard_d evaluates its leaf range:
  *   G <= D: cosets [P*D/G, (P+1)*D/G), each as in bj_lde_d;
  *   G >  D: rows [q*m, (q+1)*m) of coset i = P / (G/D), q = P mod (G/D), as an m-point coset

@@ -21,21 +21,16 @@ class CpuShardOps:
         _np(out)[:] = O.synthetic_trace(out.shape[0], log_n, col_offset=first_col)
 
     def coeffs(self, trace, out, log_n):
-        # n * monomials in bit-reversed order
-        n = 1 << log_n
+        # monomials in bit-reversed order
         for c in range(trace.shape[0]):
-            mono = O.ifft_natural_to_natural(_np(trace)[c])
-            br = O.bitreverse(mono).astype(object)
-            _np(out)[c] = np.array([(int(v) * n) % O.P for v in br], dtype=np.uint64)
+            _np(out)[c] = O.bitreverse(O.ifft_natural_to_natural(_np(trace)[c]))
 
     def lde_shard(self, coeffs, log_n, log_lde, log_shards, shard, work, lde):
         n = 1 << log_n
-        n_inv = O.gl_inv(n)
         m = (n << log_lde) >> log_shards
         cosets = O.lde_cosets(log_n, log_lde)
         for c in range(coeffs.shape[0]):
             mono = O.bitreverse(_np(coeffs)[c])
-            mono = np.array([O.gl_mul(int(v), n_inv) for v in mono], dtype=np.uint64)
             flat = np.concatenate([O.fft_natural_to_bitreversed(mono, int(s)) for s in cosets])
             _np(lde)[c] = flat[shard * m:(shard + 1) * m]
 

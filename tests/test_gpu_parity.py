@@ -91,9 +91,9 @@ def test_twiddles(bj, log_n):
         eq(bj.field.to_host(t), O.precompute_twiddles(log_n, inv))
 
 
-@pytest.mark.parametrize("log_n", [0, 1, 2, 4, 7, 11, 12, 13, 15, 20, 21])
+@pytest.mark.parametrize("log_n", [0, 1, 2, 4, 7, 11, 12, 13, 15, 17, 18, 20, 21, 23])
 def test_fft_natural_to_bitreversed_batch(bj, log_n):
-    c = 3 if log_n < 20 else 1
+    c = 3 if log_n < 18 else 1
     x = rand((c, 1 << log_n), log_n)
     x[0, 0] = np.uint64(2**64 - 1)  # non-canonical input
     for coset in (1, 7, 0x1234567):
@@ -103,7 +103,7 @@ def test_fft_natural_to_bitreversed_batch(bj, log_n):
         eq(bj.field.to_host(t), want)
 
 
-@pytest.mark.parametrize("log_n", [0, 1, 2, 3, 6, 10, 12, 13, 14, 19])
+@pytest.mark.parametrize("log_n", [0, 1, 2, 3, 6, 10, 12, 13, 14, 18, 19, 22, 23])
 def test_ifft_natural_to_natural_batch(bj, log_n):
     x = rand((2, 1 << log_n), 50 + log_n)
     for coset in (1, 7):
@@ -137,7 +137,7 @@ def test_host_seam_in_place(bj):
 # -------------------------------------------------------------------- LDE
 
 @pytest.mark.parametrize("c,log_n,log_d", [(1, 0, 1), (2, 1, 1), (3, 3, 2), (5, 6, 3), (4, 12, 1), (3, 13, 2),
-                                           (2, 16, 3), (1, 17, 1)])
+                                           (2, 16, 3), (1, 17, 1), (2, 18, 2), (1, 19, 3), (1, 20, 1)])
 def test_lde_batch(bj, c, log_n, log_d):
     x = rand((c, 1 << log_n), c * 100 + log_n)
     t = bj.field.to_device(x)
@@ -149,6 +149,35 @@ def test_lde_batch(bj, c, log_n, log_d):
     bj.fft.ifft_natural_to_natural(m, 1)
     eq(bj.field.to_host(m), m_ref)
     eq(bj.field.to_host(bj.lde.transform_monomials_to_lde(m, 1 << log_d)), l_ref)
+
+
+@pytest.mark.parametrize("log_n", [0, 1, 5, 12, 17, 18, 21])
+def test_lde_coeffs_exchange_format(bj, log_n):
+    """bj_lde_coeffs_d: monomials c_j at bitrev_n(j), canonical (the multi-GPU exchange format)."""
+    from boojum_amd._lib import call
+    c = 2
+    x = rand((c, 1 << log_n), 900 + log_n)
+    x[0, 0] = np.uint64(2**64 - 1)
+    t = bj.field.to_device(x)
+    out = bj.torch.empty_like(t)
+    call("bj_lde_coeffs_d", t.data_ptr(), c, 1 << log_n, log_n, out.data_ptr(), 1 << log_n, bj.field.stream_of(out))
+    want = np.stack([O.bitreverse(O.ifft_natural_to_natural(x[i])) for i in range(c)])
+    eq(bj.field.to_host(out), want)
+
+
+@pytest.mark.parametrize("log_n,log_d", [(18, 1), (18, 3), (23, 1)])
+def test_lde_edge_columns_large(bj, log_n, log_d):
+    """Zero / p-1 / impulse / non-canonical columns on the register-resident NTT sizes."""
+    n = 1 << log_n
+    x = np.zeros((4, n), dtype=np.uint64)
+    x[1, :] = P - 1
+    x[2, n - 1] = 1
+    x[3, :] = np.uint64(2**64 - 1)
+    t = bj.field.to_device(x)
+    l = bj.field.to_host(bj.lde.transform_raw_storages_to_lde(t, 1 << log_d))
+    m_ref, l_ref = O.lde(x, log_d, threads=8)
+    eq(l, l_ref)
+    assert not l[0].any()
 
 
 def test_lde_edge_columns(bj):

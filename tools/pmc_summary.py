@@ -1,0 +1,105 @@
+#!/usr/bin/env python3
+"""Per-launch HBM traffic and VALU counters from rocprofv3 PMC passes (scripts/profile_r1.sh).
+
+Reads <dir>/fetch, <dir>/write and <dir>/sq run_counter_collection.csv files, averages each
+counter per kernel over its dispatches and writes profiles/pmc_summary.json:
+  {config: {kernel_key: {fetch_bytes, write_bytes, hbm_bytes_per_launch, sq_insts_valu, ...}}}
+
+Units and gfx950 corrections (MI355X_MICROARCH.md, HBM section):
+* FETCH_SIZE and WRITE_SIZE are in KiB.
+* FETCH_SIZE reports half the bytes of a wide contiguous stream. That holds for the leaf kernel
+  (512 contiguous bytes per wave load; FETCH_SIZE = 16 GiB against its known 32 GiB of reads).
+  The NTT kernels read 128-byte runs, and their FETCH_SIZE equals their known byte count
+  (iNTT head: 8 GiB), so they are not doubled.
+The per-kernel factor is in READ_FACTOR; each one was calibrated on a known byte count.
+
+usage: python tools/pmc_summary.py gpurun_out/prof_TAG [--config C3]
+"""
+import argparse
+import collections
+import csv
+import json
+import os
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+# kernel-name prefix -> (key, FETCH_SIZE read factor)
+KERNELS = [
+    ("bj::leaf_hash_kernel", "leaf_hash_kernel", 2.0),
+    ("bj::node_level_kernel", "node_level_kernel", 1.0),
+    ("bj::node_tail_kernel", "node_tail_kernel", 1.0),
+    ("void bj::(anonymous namespace)::ct_head_kernel<9, 1", "ct_head_fwd", 1.0),
+    ("void bj::(anonymous namespace)::ct_head_kernel<9, 0", "ct_head_inv", 1.0),
+    ("bj::(anonymous namespace)::ct_tail_kernel", "ct_tail", 1.0),
+    ("void bj::(anonymous namespace)::dif_head_kernel<9, 1>", "dif_head_fwd", 1.0),
+    ("void bj::(anonymous namespace)::dif_head_kernel<9, 0>", "dif_head_inv", 1.0),
+    ("bj::(anonymous namespace)::dif_tail_kernel", "dif_tail", 1.0),
+]
+
+
+def key_of(name):
+    for pre, key, fac in KERNELS:
+        if name.startswith(pre):
+            return key, fac
+    return None, None
+
+
+def load(path):
+    acc = collections.defaultdict(lambda: collections.defaultdict(list))
+    if not os.path.exists(path):
+        return acc
+    per = collections.defaultdict(dict)
+    for r in csv.DictReader(open(path)):
+        per[(r["Dispatch_Id"], r["Kernel_Name"])][r["Counter_Name"]] = float(r["Counter_Value"])
+    for (_, name), ctrs in per.items():
+        k, _ = key_of(name)
+        if k:
+            for c, v in ctrs.items():
+                acc[k][c].append(v)
+    return acc
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("dir")
+    ap.add_argument("--config", default="C3")
+    ap.add_argument("--out", default=os.path.join(ROOT, "profiles", "pmc_summary.json"))
+    args = ap.parse_args()
+    data = {}
+    for sub in ("fetch", "write", "sq"):
+        for k, ctrs in load(os.path.join(args.dir, sub, "run_counter_collection.csv")).items():
+            d = data.setdefault(k, {})
+            for c, vals in ctrs.items():
+                d[c] = sum(vals) / len(vals)
+                d[c + "_dispatches"] = len(vals)
+    out = {}
+    for k, d in data.items():
+        fac = next(f for _, kk, f in KERNELS if kk == k)
+        e = {"source": os.path.basename(os.path.normpath(args.dir))}
+        if "FETCH_SIZE" in d:
+            e["fetch_bytes"] = d["FETCH_SIZE"] * 1024 * fac
+        if "WRITE_SIZE" in d:
+            e["write_bytes"] = d["WRITE_SIZE"] * 1024
+        if "fetch_bytes" in e and "write_bytes" in e:
+            e["hbm_bytes_per_launch"] = e["fetch_bytes"] + e["write_bytes"]
+        for c in ("SQ_INSTS_VALU", "SQ_WAVES", "SQ_BUSY_CYCLES", "SQ_ACTIVE_INST_VALU", "GRBM_GUI_ACTIVE"):
+            if c in d:
+                e[c.lower()] = d[c]
+        out[k] = e
+    # the LDE phase as one unit: sum of its kernels per commit (one inverse head + tail, one
+    # forward head + tail; tail launches alternate inverse / forward)
+    ct = [out.get(k) for k in ("ct_head_inv", "ct_head_fwd", "ct_tail")]
+    if all(x and "hbm_bytes_per_launch" in x for x in ct):
+        out["lde"] = {"hbm_bytes_per_launch": ct[0]["hbm_bytes_per_launch"] + ct[1]["hbm_bytes_per_launch"]
+                      + 2 * ct[2]["hbm_bytes_per_launch"], "note": "iNTT + forward, one commit"}
+    full = {}
+    if os.path.exists(args.out):
+        full = json.load(open(args.out))
+    full[args.config] = out
+    with open(args.out, "w") as f:
+        json.dump(full, f, indent=1, sort_keys=True)
+    print(json.dumps(out, indent=1, sort_keys=True))
+
+
+if __name__ == "__main__":
+    main()

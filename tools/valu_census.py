@@ -1,0 +1,112 @@
+#!/usr/bin/env python3
+"""Static VALU census of one Poseidon2 permutation as compiled for gfx950.
+
+The permutation (csrc/poseidon2.hpp) has three `#pragma unroll 1` round loops with fixed
+trip counts: 4 full rounds, 22 partial rounds and 4 full rounds. `node_level_kernel`
+(csrc/merkle.hip) runs exactly one permutation per lane, so its dynamic instruction
+stream is known statically:
+    straight-line code x1 + loop bodies x (4, 22, 4).
+This tool disassembles the gfx950 code object and weights each VALU instruction by the
+issue cost measured in profiles/r1_isa_rates.txt:
+* 1 slot: full-rate 32-bit ops (v_add_u32, v_mov_b32, logic);
+* 2 slots: carry, 64-bit and multiply ops.
+The output is the issue-slot count per permutation, which bench.py uses for the leaf
+kernel's VALU roofline.
+
+usage: python tools/valu_census.py [--json out.json]
+"""
+import argparse
+import json
+import os
+import re
+import subprocess
+import sys
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+LLVM = "/opt/rocm/lib/llvm/bin"
+HIPCC = "/opt/rocm/bin/hipcc"
+
+FULL_RATE = re.compile(r"^v_(add_u32|sub_u32|mov_b32|and_b32|or_b32|xor_b32|lshlrev_b32|lshrrev_b32|"
+                       r"alignbit_b32|bfe_u32|and_or_b32|or3_b32|xad_u32|not_b32|cndmask_b32_e32)")
+
+
+def disassemble():
+    src = os.path.join(ROOT, "era-boojum_amd", "csrc", "merkle.hip")
+    dev = "/tmp/_census_merkle_dev.o"
+    co = "/tmp/_census_merkle.co"
+    subprocess.run([HIPCC, "-O3", "-std=c++17", "--offload-arch=gfx950", "--cuda-device-only", "-c", "-o", dev,
+                    src], check=True)
+    subprocess.run([os.path.join(LLVM, "clang-offload-bundler"), "--unbundle", "--type=o", "--input=" + dev,
+                    "--targets=hipv4-amdgcn-amd-amdhsa--gfx950", "--output=" + co], check=True)
+    return subprocess.run([os.path.join(LLVM, "llvm-objdump"), "-d", co], check=True, capture_output=True,
+                          text=True).stdout
+
+
+def kernel_lines(dis, name):
+    out, on = [], False
+    for line in dis.splitlines():
+        if line.endswith(">:"):
+            on = name in line
+            continue
+        if on and line.strip():
+            out.append(line)
+    return out
+
+
+def parse(lines):
+    """[(addr, mnemonic, branch_target_addr|None)]"""
+    instrs = []
+    for line in lines:
+        m = re.match(r"\s+(\S+).*//\s*([0-9A-Fa-f]+):", line)
+        if not m:
+            continue
+        mn, addr = m.group(1), int(m.group(2), 16)
+        tgt = None
+        t = re.search(r"<[^+>]+\+0x([0-9a-f]+)>", line)
+        if mn.startswith("s_cbranch") or mn == "s_branch":
+            if t:
+                tgt = int(t.group(1), 16)
+        instrs.append((addr, mn, tgt))
+    return instrs
+
+
+def census(instrs, trips=(4, 22, 4)):
+    base = instrs[0][0]
+    back = [(i, a, t) for i, (a, mn, t) in enumerate(instrs) if t is not None and base + t < a]
+    if len(back) != len(trips):
+        raise SystemExit("expected %d backward branches, found %d" % (len(trips), len(back)))
+    weight = [1] * len(instrs)
+    for (i_end, _, t), trip in zip(back, trips):
+        start = next(k for k, (a, _, _) in enumerate(instrs) if a == base + t)
+        for k in range(start, i_end + 1):
+            weight[k] = trip
+    valu = slots = 0
+    hist = {}
+    for (a, mn, _), w in zip(instrs, weight):
+        if not mn.startswith("v_"):
+            continue
+        cost = 1 if FULL_RATE.match(mn) else 2
+        valu += w
+        slots += w * cost
+        hist[mn] = hist.get(mn, 0) + w
+    return valu, slots, hist
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--json")
+    args = ap.parse_args()
+    dis = disassemble()
+    instrs = parse(kernel_lines(dis, "node_level_kernel"))
+    valu, slots, hist = census(instrs)
+    res = {"kernel": "node_level_kernel (one Poseidon2 permutation per lane + 64 B in / 32 B out)",
+           "valu_instr_per_perm": valu, "issue_slots_per_perm": slots,
+           "top": dict(sorted(hist.items(), key=lambda kv: -kv[1])[:12])}
+    print(json.dumps(res, indent=1))
+    if args.json:
+        with open(args.json, "w") as f:
+            json.dump(res, f, indent=1)
+
+
+if __name__ == "__main__":
+    main()
