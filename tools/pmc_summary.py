@@ -7,11 +7,12 @@ counter per kernel over its dispatches and writes profiles/pmc_summary.json:
 
 Units and gfx950 corrections (MI355X_MICROARCH.md, HBM section):
 * FETCH_SIZE and WRITE_SIZE are in KiB.
-* FETCH_SIZE reports half the bytes of a wide contiguous stream. That holds for the leaf kernel
-  (512 contiguous bytes per wave load; FETCH_SIZE = 16 GiB against its known 32 GiB of reads).
-  The NTT kernels read 128-byte runs, and their FETCH_SIZE equals their known byte count
+* FETCH_SIZE reports half the bytes of a wide contiguous stream. That holds for the leaf kernel and the NTT tails
+  (512 contiguous bytes per wave load; leaf: FETCH_SIZE = 16 GiB against its known 32 GiB of reads;
+  tails: the inverse + forward average 10.1 GiB against a known 20 GiB).
+  The NTT heads read 128-byte runs, and their FETCH_SIZE equals their known byte count
   (iNTT head: 8 GiB), so they are not doubled.
-The per-kernel factor is in READ_FACTOR; each one was calibrated on a known byte count.
+The per-kernel factor is the third field of KERNELS; each was calibrated on a known byte count.
 
 usage: python tools/pmc_summary.py gpurun_out/prof_TAG [--config C3]
 """
@@ -30,10 +31,10 @@ KERNELS = [
     ("bj::node_tail_kernel", "node_tail_kernel", 1.0),
     ("void bj::(anonymous namespace)::ct_head_kernel<9, 1", "ct_head_fwd", 1.0),
     ("void bj::(anonymous namespace)::ct_head_kernel<9, 0", "ct_head_inv", 1.0),
-    ("bj::(anonymous namespace)::ct_tail_kernel", "ct_tail", 1.0),
+    ("bj::(anonymous namespace)::ct_tail_kernel", "ct_tail", 2.0),
     ("void bj::(anonymous namespace)::dif_head_kernel<9, 1>", "dif_head_fwd", 1.0),
     ("void bj::(anonymous namespace)::dif_head_kernel<9, 0>", "dif_head_inv", 1.0),
-    ("bj::(anonymous namespace)::dif_tail_kernel", "dif_tail", 1.0),
+    ("bj::(anonymous namespace)::dif_tail_kernel", "dif_tail", 2.0),
 ]
 
 
