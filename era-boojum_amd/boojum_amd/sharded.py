@@ -1,24 +1,35 @@
 """Coset-sharded witness commitment across G GPUs (one process per GPU, RCCL over xGMI).
 
 The reference runs the whole commitment on one host (prover.rs:313-353 with the Worker
-pool); this is its multi-GPU split (BASELINE north_star):
+pool). This is its multi-GPU split (BASELINE north_star):
 
-  * the trace is column-sharded: rank P holds columns [P*C/G, (P+1)*C/G);
+  * the trace is column-sharded: every rank holds C/G of the columns;
   * each rank inverse-transforms its own columns into the exchange format
-    (bj_lde_coeffs_d: monomials in bit-reversed order), straight into its slice of
-    the all-columns coefficient buffer;
-  * one all-gather (RCCL, in place) gives every rank every column's coefficients
-    (8 n C bytes in total) -- the only data-path exchange;
+    (bj_lde_coeffs_d: monomials in bit-reversed order), straight into its slice of the
+    all-columns coefficient buffer;
+  * all-gathers (RCCL, in place) give every rank every column's coefficients
+    (8 n C bytes in total). They are the only data-path exchange;
   * rank P evaluates its contiguous range of m = n*D/G leaves of the flat leaf domain
     (coset * n + row, merkle_tree.rs:112-157): whole cosets when G <= D, a folded sub-coset
     when G > D (bj_lde_shard_d);
-  * leaves and the subtree over them are hashed locally (contiguous aligned leaf ranges are
-    subtrees of the reference's tree, so every node is the reference's node);
-  * the cap is all-gathered: cap/G digests per rank when cap >= G; otherwise every rank
+  * leaves and the subtree over them are hashed locally. Contiguous aligned leaf ranges are
+    subtrees of the reference's tree, so every node is the reference's node;
+  * the cap is all-gathered: cap/G digests per rank when cap >= G. Otherwise every rank
     all-gathers the G subtree roots and hashes the top log2(G/cap) levels redundantly.
 
+Column pipeline (C a multiple of 8 G). The leaf sponge absorbs columns in order, 8 per
+permutation, and between 8-column groups its only carried state is the 4 capacity words
+(bj_merkle_leaves_partial_d). So the columns are dealt to ranks in 8-column blocks, and the
+exchange runs as one all-gather per chunk of b blocks per rank (8 b G consecutive columns).
+All chunks' all-gathers are issued up front on RCCL's stream. Chunk k's coset transform and
+sponge absorption then run on the compute stream as soon as chunk k has arrived, while later
+chunks are still on the wire. Block ownership: global 8-column block k*b*G + P*b + j
+(chunk k, j < b) belongs to rank P, at local block k*b + j. Otherwise (C not a multiple of
+8 G) rank P holds the contiguous columns [P*C/G, (P+1)*C/G) and one all-gather runs
+before the transforms.
+
 Outputs stay sharded: each rank keeps its LDE slice, its leaves and subtree nodes, and
-the full cap.  The compute steps are an `ops` object: `HipShardOps` (the C ABI on the
+the full cap. The compute steps are an `ops` object: `HipShardOps` (the C ABI on the
 GPU) is the product path and the default; the CPU multi-process tests inject a CPU
 implementation to check the orchestration with `gloo`.
 """
@@ -26,6 +37,8 @@ import torch
 
 from ._lib import call
 from .field import stream_of
+
+CHUNK_TARGET_COLS = 64   # columns per pipelined all-gather chunk (at least 8 G)
 
 
 def _log2(n):
@@ -45,9 +58,10 @@ class HipShardOps:
         call("bj_lde_shard_d", coeffs.data_ptr(), coeffs.shape[0], coeffs.stride(0), log_n, log_lde, log_shards,
              shard, None if work is None else work.data_ptr(), lde.data_ptr(), stream_of(lde))
 
-    def leaves(self, lde, out):
+    def leaves(self, lde, out, cap_in=None, final=True):
         c, m = lde.shape
-        call("bj_merkle_leaves_d", lde.data_ptr(), c, lde.stride(0), m, out.data_ptr(), stream_of(out))
+        call("bj_merkle_leaves_partial_d", lde.data_ptr(), c, lde.stride(0), m,
+             None if cap_in is None else cap_in.data_ptr(), out.data_ptr(), 1 if final else 0, stream_of(out))
 
     def nodes(self, leaves, cap_size, out):
         call("bj_merkle_nodes_d", leaves.data_ptr(), leaves.shape[0], cap_size, out.data_ptr(), stream_of(out))
@@ -57,30 +71,47 @@ class HipShardOps:
              stream_of(out))
 
 
-def _all_gather(out, inp, group=None):
-    """out (G*k, ...) <- concat over ranks of inp (k, ...).  RCCL (backend "nccl") runs in
-    place on device memory; gloo (the CPU tests) stages device tensors through the host."""
+class _Done:
+    def wait(self):
+        pass
+
+
+def _all_gather(out, inp, group=None, async_op=False):
+    """out (G*k, ...) <- concat over ranks of inp (k, ...). RCCL (backend "nccl") runs in
+    place on device memory and, with async_op, returns a handle whose wait() orders the
+    current stream after it. gloo (the CPU tests) stages through the host synchronously."""
     import torch.distributed as dist
     if dist.get_backend(group) == "nccl":
-        dist.all_gather_into_tensor(out, inp, group=group)
-        return
+        w = dist.all_gather_into_tensor(out, inp, group=group, async_op=async_op)
+        return w if async_op else None
     world = dist.get_world_size(group)
     src = inp.detach().cpu().contiguous()
     parts = [torch.empty_like(src) for _ in range(world)]
     dist.all_gather(parts, src, group=group)
     out.copy_(torch.cat(parts, 0).to(out.device))
+    return _Done() if async_op else None
+
+
+class _NoTimer:
+    def start(self, name):
+        pass
+
+    def stop(self, name):
+        pass
 
 
 class ShardedWorkspace:
     """Per-rank HBM buffers of a G-way sharded commit of C x 2^log_n at LDE 2^log_lde.
 
-    coeffs (C, n)             all columns' coefficients (this rank's slice written locally)
-    work   (C, m) | None      fold scratch (G > D only)
+    coeffs (C, n)             all columns' coefficients (this rank's slices written locally)
+    work   (K, m) | None      fold scratch, K = columns per chunk (G > D only)
     lde    (C, m)             this rank's leaf range of every column's LDE, m = n*D/G
+    state  (m, 4) | None      carried sponge capacity between column chunks
     leaves (m, 4), nodes (m - cap_local, 4), cap (cap, 4)
     """
 
-    def __init__(self, n_cols, log_n, log_lde, cap_size, rank, world, device="cuda", group=None, ops=None):
+    def __init__(self, n_cols, log_n, log_lde, cap_size, rank, world, device="cuda", group=None, ops=None,
+                 chunk_cols=CHUNK_TARGET_COLS):
         log_g = _log2(world)
         _log2(cap_size)
         if n_cols % world:
@@ -100,10 +131,23 @@ class ShardedWorkspace:
         self.cap_local = max(1, cap_size // world)
         if m <= self.cap_local:
             raise ValueError("each shard needs more leaves than its cap slice")
+        # column pipeline geometry
+        self.pipelined = n_cols % (8 * world) == 0
+        if self.pipelined:
+            blocks_per_rank = n_cols // (8 * world)
+            b = max(1, chunk_cols // (8 * world))
+            while blocks_per_rank % b:
+                b -= 1
+            self.b = b
+            self.n_chunks = blocks_per_rank // b
+            self.chunk_cols = 8 * b * world
+        else:
+            self.b, self.n_chunks, self.chunk_cols = None, 1, n_cols
         kw = dict(dtype=torch.int64, device=device)
         self.coeffs = torch.empty((n_cols, n), **kw)
-        self.work = torch.empty((n_cols, m), **kw) if log_g > log_lde else None
+        self.work = torch.empty((self.chunk_cols, m), **kw) if log_g > log_lde else None
         self.lde = torch.empty((n_cols, m), **kw)
+        self.state = torch.empty((m, 4), **kw) if self.n_chunks > 1 else None
         self.leaves = torch.empty((m, 4), **kw)
         self.nodes = torch.empty((m - self.cap_local, 4), **kw)
         self.cap = torch.empty((cap_size, 4), **kw)
@@ -115,10 +159,17 @@ class ShardedWorkspace:
         elif self.coeffs.is_cuda:
             call("bj_prepare", log_n)
 
+    def column_runs(self):
+        """This rank's columns as (local_first, global_first, count) runs, in local order."""
+        P = self.rank
+        if not self.pipelined:
+            return [(0, P * self.cols_per_rank, self.cols_per_rank)]
+        run = 8 * self.b
+        return [(k * run, k * self.chunk_cols + P * run, run) for k in range(self.n_chunks)]
+
     @property
     def my_columns(self):
-        c0 = self.rank * self.cols_per_rank
-        return c0, c0 + self.cols_per_rank
+        return [g + i for _, g, c in self.column_runs() for i in range(c)]
 
     @property
     def leaf_range(self):
@@ -127,31 +178,47 @@ class ShardedWorkspace:
     def synthetic_trace_shard(self):
         """This rank's columns of the synthetic trace, generated in place."""
         t = torch.empty((self.cols_per_rank, 1 << self.log_n), dtype=torch.int64, device=self.coeffs.device)
-        self.ops.synthetic(t, self.log_n, self.my_columns[0])
+        for lo, g, c in self.column_runs():
+            self.ops.synthetic(t[lo:lo + c], self.log_n, g)
         return t
 
 
-def sharded_witness_commit(trace_shard, ws, marks=None):
-    """Commit this rank's column shard (C/G, n) into `ws`; collective over ws.group.
+def sharded_witness_commit(trace_shard, ws, timer=None):
+    """Commit this rank's column shard (C/G, n; columns in ws.my_columns order) into `ws`.
+    Collective over ws.group.
 
-    `marks`, if given, is called with a phase name after each phase is enqueued
-    ("ifft", "exchange", "lde", "leaves", "nodes") -- the bench records events there."""
+    `timer`, if given, has start(name) / stop(name) called around the compute steps
+    ("ifft", "lde", "leaves", "nodes"); the bench records events there."""
     ops = ws.ops
-    mark = marks or (lambda name: None)
-    c0, c1 = ws.my_columns
+    timer = timer or _NoTimer()
     if tuple(trace_shard.shape) != (ws.cols_per_rank, 1 << ws.log_n):
         raise ValueError("trace shard must be (%d, %d)" % (ws.cols_per_rank, 1 << ws.log_n))
-    mine = ws.coeffs[c0:c1]
-    ops.coeffs(trace_shard, mine, ws.log_n)
-    mark("ifft")
-    if ws.world > 1:
-        _all_gather(ws.coeffs, mine, ws.group)
-    mark("exchange")
-    ops.lde_shard(ws.coeffs, ws.log_n, ws.log_lde, ws.log_g, ws.rank, ws.work, ws.lde)
-    mark("lde")
-    ops.leaves(ws.lde, ws.leaves)
-    mark("leaves")
+    runs = ws.column_runs()
+    timer.start("ifft")
+    for lo, g, c in runs:
+        ops.coeffs(trace_shard[lo:lo + c], ws.coeffs[g:g + c], ws.log_n)
+    timer.stop("ifft")
+    K = ws.chunk_cols
+    handles = []
+    for k, (lo, g, c) in enumerate(runs):
+        if ws.world > 1:
+            handles.append(_all_gather(ws.coeffs[k * K:(k + 1) * K], ws.coeffs[g:g + c], ws.group, async_op=True))
+        else:
+            handles.append(_Done())
+    for k in range(ws.n_chunks):
+        handles[k].wait()
+        cols = slice(k * K, (k + 1) * K)
+        work = None if ws.work is None else ws.work[:K]
+        timer.start("lde")
+        ops.lde_shard(ws.coeffs[cols], ws.log_n, ws.log_lde, ws.log_g, ws.rank, work, ws.lde[cols])
+        timer.stop("lde")
+        last = k == ws.n_chunks - 1
+        timer.start("leaves")
+        ops.leaves(ws.lde[cols], ws.leaves if last else ws.state, cap_in=None if k == 0 else ws.state, final=last)
+        timer.stop("leaves")
+    timer.start("nodes")
     ops.nodes(ws.leaves, ws.cap_local, ws.nodes)
+    timer.stop("nodes")
     local_cap = ws.nodes[-ws.cap_local:]
     if ws.cap_size >= ws.world:
         if ws.world > 1:
@@ -162,5 +229,4 @@ def sharded_witness_commit(trace_shard, ws, marks=None):
         _all_gather(ws.roots, local_cap, ws.group)
         ops.nodes(ws.roots, ws.cap_size, ws.top_nodes)
         ws.cap.copy_(ws.top_nodes[-ws.cap_size:])
-    mark("nodes")
     return ws

@@ -469,6 +469,17 @@ int bj_merkle_leaves_d(const uint64_t* src, uint32_t n_cols, size_t col_stride, 
     return BJ_OK;
 }
 
+int bj_merkle_leaves_partial_d(const uint64_t* src, uint32_t n_cols, size_t col_stride, size_t n_leaves,
+                               const uint64_t* cap_in, uint64_t* out, int final_, void* stream) {
+    if (!final_ && (n_cols & 7))
+        return fail(BJ_EINVAL, "a non-final column range must be a multiple of the sponge rate (8)");
+    if (final_ && cap_in && n_cols == 0)
+        return fail(BJ_EINVAL, "the final column range of a continued sponge must be non-empty");
+    HIP_TRY(bj::launch_leaves_partial(src, col_stride, n_cols, n_leaves, cap_in, out, final_ != 0, S(stream)),
+            "leaves");
+    return BJ_OK;
+}
+
 int bj_merkle_nodes_d(const uint64_t* leaves, size_t n_leaves, uint32_t cap_size, uint64_t* nodes, void* stream) {
     if (!is_pow2(n_leaves) || !is_pow2(cap_size) || n_leaves <= cap_size)
         return fail(BJ_EINVAL, "need power-of-two n_leaves > cap_size (merkle_tree.rs:83-96)");

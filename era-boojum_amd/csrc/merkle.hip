@@ -46,15 +46,29 @@ __device__ __forceinline__ void load8(p2::State& s, const uint64_t* q, size_t st
     }
 }
 
+// HAS_IN: the sponge continues from carried capacity words cap_in[L][0..4] = state[8..12]
+// (the Overwrite sponge's rate words are overwritten by the next absorption, so the
+// capacity is the whole carried state between 8-element groups).  FINAL: write the digest
+// state[0..4]; otherwise write the capacity state[8..12] for the next column range.
+template <bool HAS_IN, bool FINAL>
 __global__ __launch_bounds__(LEAF_THREADS) void leaf_hash_kernel(const uint64_t* __restrict__ src,
                                                                  size_t col_stride, uint32_t n_cols,
-                                                                 size_t n_leaves, uint64_t* __restrict__ out) {
+                                                                 size_t n_leaves, const uint64_t* cap_in,
+                                                                 uint64_t* out) {
     const size_t L = blockIdx.x * (size_t)LEAF_THREADS + threadIdx.x;
     if (L >= n_leaves) return;
     const uint64_t* p = src + L;
     p2::State s;
 #pragma unroll
     for (int i = 0; i < 12; i++) s.lo[i] = s.hi[i] = 0;
+    if (HAS_IN) {
+#pragma unroll
+        for (int i = 0; i < 4; i++) {
+            const uint64_t v = cap_in[4 * L + i];
+            s.lo[8 + i] = (uint32_t)v;
+            s.hi[8 + i] = (uint32_t)(v >> 32);
+        }
+    }
     const uint32_t full = n_cols >> 3;
     const uint32_t rem = n_cols & 7;
     // software prefetch: the next group's 8 loads are issued before this group's permute
@@ -76,11 +90,12 @@ __global__ __launch_bounds__(LEAF_THREADS) void leaf_hash_kernel(const uint64_t*
         }
         p2::permute(s);
     }
-    if (rem) {
+    if (FINAL && rem) {
         load8(s, p + (size_t)full * 8 * col_stride, col_stride, rem);
         p2::permute(s);
     }
-    store_canon4(s, out + 4 * L);
+    if (FINAL) store_canon4(s, out + 4 * L);
+    else store_canon4_at(s, 2, out + 4 * L);
 }
 
 __device__ __forceinline__ void node_hash(const uint64_t* l, const uint64_t* r, uint64_t* o) {
@@ -154,10 +169,24 @@ __global__ __launch_bounds__(256) void permute_kernel(uint64_t* states, size_t c
 
 hipError_t launch_leaves(const uint64_t* src, size_t col_stride, uint32_t n_cols, size_t n_leaves, uint64_t* out,
                          hipStream_t st) {
+    return launch_leaves_partial(src, col_stride, n_cols, n_leaves, nullptr, out, true, st);
+}
+
+hipError_t launch_leaves_partial(const uint64_t* src, size_t col_stride, uint32_t n_cols, size_t n_leaves,
+                                 const uint64_t* cap_in, uint64_t* out, bool final_, hipStream_t st) {
     if (n_leaves == 0) return hipSuccess;
-    size_t blocks = (n_leaves + LEAF_THREADS - 1) / LEAF_THREADS;
-    hipLaunchKernelGGL(leaf_hash_kernel, dim3((unsigned)blocks), dim3(LEAF_THREADS), 0, st, src, col_stride,
-                       n_cols, n_leaves, out);
+    const dim3 g((unsigned)((n_leaves + LEAF_THREADS - 1) / LEAF_THREADS));
+#define BJ_LEAF(IN, FIN) \
+    hipLaunchKernelGGL((leaf_hash_kernel<IN, FIN>), g, dim3(LEAF_THREADS), 0, st, src, col_stride, n_cols, n_leaves, \
+                       cap_in, out)
+    if (cap_in) {
+        if (final_) BJ_LEAF(true, true);
+        else BJ_LEAF(true, false);
+    } else {
+        if (final_) BJ_LEAF(false, true);
+        else BJ_LEAF(false, false);
+    }
+#undef BJ_LEAF
     return hipGetLastError();
 }
 

@@ -144,6 +144,18 @@ int bj_hash_into_node_h(const uint64_t* left4, const uint64_t* right4, uint64_t*
 int bj_merkle_leaves_d(const uint64_t* src, uint32_t n_cols, size_t col_stride, size_t n_leaves,
                        uint64_t* leaves, void* stream);
 
+/* Leaf hashing over a column range, continuing a sponge (the column-pipelined multi-GPU
+ * commit absorbs column chunks as they arrive).  The Overwrite sponge replaces the rate words
+ * with each 8-element group, so between groups its whole carried state is the capacity
+ * state[8..12].  cap_in: NULL for a fresh sponge (zero state), else n_leaves x 4 capacity words
+ * from a previous non-final call.  final_ == 0: n_cols must be a multiple of 8; out receives
+ * the capacity words (n_leaves x 4, canonical).  final_ != 0: the remaining columns are
+ * absorbed with the reference's padding (sponge.rs:300-323) and out receives the digests, as
+ * bj_merkle_leaves_d.  cap_in == out is allowed.  Chaining calls over columns [0, k), [k, C)
+ * gives exactly bj_merkle_leaves_d over [0, C). */
+int bj_merkle_leaves_partial_d(const uint64_t* src, uint32_t n_cols, size_t col_stride, size_t n_leaves,
+                               const uint64_t* cap_in, uint64_t* out, int final_, void* stream);
+
 /* continue_from_leaf_hashes (merkle_tree.rs:388-449): node levels from n_leaves leaves
  * up to cap_size nodes.  nodes: (n_leaves - cap_size) x 4, the levels concatenated from
  * the leaves upward (node_hashes_enumerated_from_leafs); the cap is the last cap_size

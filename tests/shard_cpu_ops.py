@@ -34,9 +34,29 @@ class CpuShardOps:
             flat = np.concatenate([O.fft_natural_to_bitreversed(mono, int(s)) for s in cosets])
             _np(lde)[c] = flat[shard * m:(shard + 1) * m]
 
-    def leaves(self, lde, out):
+    def leaves(self, lde, out, cap_in=None, final=True):
         src = _np(lde)
-        _np(out)[:] = np.stack([O.hash_into_leaf(np.ascontiguousarray(src[:, r])) for r in range(src.shape[1])])
+        if cap_in is None and final:
+            _np(out)[:] = np.stack([O.hash_into_leaf(np.ascontiguousarray(src[:, r])) for r in range(src.shape[1])])
+            return
+        # the Overwrite sponge continued from carried capacity words (sponge.rs:224-323)
+        cin = None if cap_in is None else _np(cap_in).copy()
+        res = np.zeros((src.shape[1], 4), dtype=np.uint64)
+        for r in range(src.shape[1]):
+            st = np.zeros(12, dtype=np.uint64)
+            if cin is not None:
+                st[8:] = cin[r]
+            col = src[:, r]
+            full, rem = divmod(col.shape[0], 8)
+            for g in range(full):
+                st[:8] = col[8 * g: 8 * g + 8]
+                st = O.poseidon2_permutation(st)
+            if final and rem:
+                st[:8] = 0
+                st[:rem] = col[8 * full:]
+                st = O.poseidon2_permutation(st)
+            res[r] = st[:4] if final else st[8:]
+        _np(out)[:] = res
 
     def nodes(self, leaves, cap_size, out):
         lv = _np(leaves)

@@ -18,14 +18,15 @@ def run(rank, world, port, cfg, outdir, device, paths):
     dist.init_process_group("gloo", rank=rank, world_size=world)
     try:
         from boojum_amd.sharded import ShardedWorkspace, sharded_witness_commit
-        n_cols, log_n, log_lde, cap = cfg
+        n_cols, log_n, log_lde, cap = cfg[:4]
+        extra = {"chunk_cols": cfg[4]} if len(cfg) > 4 else {}
         if device == "cpu":
             from shard_cpu_ops import CpuShardOps
             ops, dev = CpuShardOps(), "cpu"
         else:
             torch.cuda.set_device(0)
             ops, dev = None, "cuda:0"
-        ws = ShardedWorkspace(n_cols, log_n, log_lde, cap, rank, world, device=dev, ops=ops)
+        ws = ShardedWorkspace(n_cols, log_n, log_lde, cap, rank, world, device=dev, ops=ops, **extra)
         tr = ws.synthetic_trace_shard()
         sharded_witness_commit(tr, ws)
         if dev != "cpu":

@@ -23,7 +23,7 @@ def run_and_check(world, cfg, tmp_path, device):
     import shard_worker
     mp.start_processes(shard_worker.run, args=(world, free_port(), cfg, str(tmp_path), device, PATHS), nprocs=world,
                        join=True, start_method="spawn")
-    n_cols, log_n, log_lde, cap = cfg
+    n_cols, log_n, log_lde, cap = cfg[:4]
     n, nl = 1 << log_n, 1 << (log_n + log_lde)
     m = nl // world
     ref = O.lde_commit(O.synthetic_trace(n_cols, log_n), log_lde, cap, threads=4)

@@ -221,6 +221,36 @@ def test_merkle_tree(bj, c, nl, cap):
         assert bj.merkle.MerkleTreeWithCap.verify_proof_over_cap(path, tree.get_cap(), leaf, idx)
 
 
+@pytest.mark.parametrize("c,splits", [(16, [8]), (37, [8, 24]), (256, [64, 128, 192]), (9, [8]), (24, [16])])
+def test_leaves_partial_chain_equals_full(bj, c, splits):
+    """bj_merkle_leaves_partial_d over column ranges, carrying the capacity, == bj_merkle_leaves_d."""
+    from boojum_amd._lib import call
+    nl = 1000
+    src = rand((c, nl), c * 7 + len(splits))
+    t = bj.field.to_device(src)
+    st = bj.field.stream_of(t)
+    full = bj.torch.empty((nl, 4), dtype=bj.torch.int64, device=t.device)
+    call("bj_merkle_leaves_d", t.data_ptr(), c, nl, nl, full.data_ptr(), st)
+    state = bj.torch.empty((nl, 4), dtype=bj.torch.int64, device=t.device)
+    out = bj.torch.empty((nl, 4), dtype=bj.torch.int64, device=t.device)
+    bounds = [0] + splits + [c]
+    for i in range(len(bounds) - 1):
+        a, b = bounds[i], bounds[i + 1]
+        last = i == len(bounds) - 2
+        call("bj_merkle_leaves_partial_d", t[a:b].data_ptr(), b - a, nl, nl, None if i == 0 else state.data_ptr(),
+             (out if last else state).data_ptr(), 1 if last else 0, st)
+    eq(bj.field.to_host(out), bj.field.to_host(full))
+    want = np.stack([O.hash_into_leaf(np.ascontiguousarray(src[:, r])) for r in (0, 1, nl - 1)])
+    eq(bj.field.to_host(out)[[0, 1, nl - 1]], want)
+
+
+def test_leaves_partial_rejects_ragged_middle(bj):
+    from boojum_amd import BoojumError
+    from boojum_amd._lib import call
+    with pytest.raises(BoojumError):
+        call("bj_merkle_leaves_partial_d", None, 7, 1, 1, None, None, 0, None)
+
+
 # --------------------------------------------------------------- commit
 
 @pytest.mark.parametrize("c,log_n,log_d,cap", [(32, 16, 1, 16), (7, 10, 2, 8), (9, 9, 3, 16), (1, 4, 1, 2)])

@@ -1,8 +1,9 @@
 """Multi-process (gloo, CPU) tests of the coset-sharded commit orchestration
 (boojum_amd/sharded.py) with the oracle standing in for the HIP steps: column-shard
-ownership, the coefficient all-gather order, leaf-range ownership for G <= D (whole
-cosets) and G > D (sub-cosets), subtree nodes as slices of the reference tree, and cap
-assembly for cap >= G and cap < G (top levels hashed redundantly)."""
+ownership (contiguous, and 8-column blocks for the column pipeline), the coefficient
+all-gather order, leaf-range ownership for G <= D (whole cosets) and G > D (sub-cosets),
+the sponge carried across column chunks, subtree nodes as slices of the reference tree, and
+cap assembly for cap >= G and cap < G (top levels hashed redundantly)."""
 import pytest
 
 from sharded_check import run_and_check
@@ -13,6 +14,9 @@ from sharded_check import run_and_check
     (2, (2, 4, 2, 2)),    # G < D
     (4, (4, 4, 1, 2)),    # G > D (sub-cosets), cap < G
     (4, (8, 5, 2, 16)),   # G == D, cap > G
+    (2, (32, 5, 1, 4, 16)),   # column pipeline: 2 chunks of 16 columns, G == D
+    (4, (64, 4, 1, 2, 32)),   # column pipeline: 2 chunks, G > D (sub-cosets), cap < G
+    (2, (48, 4, 2, 8, 16)),   # column pipeline: 3 chunks, G < D
 ])
 def test_sharded_commit_gloo(world, cfg, tmp_path):
     run_and_check(world, cfg, tmp_path, "cpu")
