@@ -64,3 +64,56 @@ def synthetic_trace(n_cols, log_n, seed=42, first_col=0, device="cuda", out=None
     t = out if out is not None else torch.empty((n_cols, n), dtype=torch.int64, device=device)
     call("bj_fill_synthetic_d", t.data_ptr(), n_cols, n, log_n, seed, first_col, stream_of(t))
     return t
+
+
+# ------------------------------------------------------------------ other oracles
+# The prover's other commitments go through the same kernels; only the column sets and the
+# LDE degree vs committed cosets differ.  The reference computes every LDE at
+# used_lde_degree = max(fri_lde_factor, quotient_degree) (prover.rs:313) and commits only the
+# first fri_lde_factor cosets of each column (subset_for_degree, lde.rs:298-308).
+
+
+class OracleCommitment:
+    """An LDE (C, D, n) on device and the MerkleTreeWithCap over its first k cosets."""
+
+    def __init__(self, lde, tree):
+        self.lde = lde
+        self.tree = tree
+
+    def get_cap(self):
+        return self.tree.get_cap()
+
+
+def commit_trace_columns(trace, lde_degree, fri_lde_factor, cap_size):
+    """Base-field columns (C, n) in Lagrange (trace) form: iFFT, coset LDE at lde_degree, tree
+    over the first fri_lde_factor cosets.  The witness oracle (prover.rs:316-347) and the setup
+    oracle (setup.rs:1146-1204, setup_storage.rs:18-70) are this call."""
+    from .lde import transform_raw_storages_to_lde
+    from .merkle import MerkleTreeWithCap
+    if fri_lde_factor > lde_degree:
+        raise ValueError("fri_lde_factor exceeds the LDE degree")
+    lde = transform_raw_storages_to_lde(trace, lde_degree)
+    return OracleCommitment(lde, MerkleTreeWithCap.construct(lde, cap_size, num_cosets=fri_lde_factor))
+
+
+def second_stage_commit(z_poly, intermediate_polys, lookup_witness_encoding_polys,
+                        lookup_multiplicities_encoding_polys, lde_degree, fri_lde_factor, cap_size):
+    """SecondStageProductsStorage::from_base_trace_ext + the stage-2 tree (prover.rs:505-554).
+    Every argument is a GoldilocksExt2 polynomial as a (c0, c1) pair of (n,) base columns in
+    Lagrange form (or a list of such pairs); the leaf order is z, intermediates, lookup witness
+    encodings, multiplicity encodings, each as c0 then c1 (prover.rs:520-547)."""
+    cols = [z_poly[0], z_poly[1]]
+    for group in (intermediate_polys, lookup_witness_encoding_polys, lookup_multiplicities_encoding_polys):
+        for c0, c1 in group:
+            cols += [c0, c1]
+    trace = torch.stack([torch.as_tensor(c) for c in cols])
+    return commit_trace_columns(trace, lde_degree, fri_lde_factor, cap_size)
+
+
+def quotient_commit(monomials, fri_lde_factor, cap_size):
+    """Quotient chunks already in monomial form (prover.rs:1454-1495): transform_monomials_to_lde
+    at fri_lde_factor, then the tree over all its cosets."""
+    from .lde import transform_monomials_to_lde
+    from .merkle import MerkleTreeWithCap
+    lde = transform_monomials_to_lde(monomials, fri_lde_factor)
+    return OracleCommitment(lde, MerkleTreeWithCap.construct(lde, cap_size))

@@ -98,6 +98,52 @@ class MerkleTreeWithCap:
         call("bj_merkle_nodes_d", leaves.data_ptr(), nl, cap_size, nodes.data_ptr(), st)
         return cls(cap_size, leaves, nodes)
 
+    @classmethod
+    def construct_by_chunking(cls, leafs_sources, elements_to_take_per_leaf, cap_size):
+        """merkle_tree.rs:176-306 (the FRI base oracle, fri/mod.rs:179-187): leaf j of the flat
+        tree hashes, for each source in order, elements [j*E, (j+1)*E) of its flat LDE (cosets
+        in order). leafs_sources: (C, D, n) LDE tensor or (C, L) flat rows."""
+        src, c, stride, total = _leaf_sources(leafs_sources)
+        e = elements_to_take_per_leaf
+        _log2(e)
+        _log2(cap_size)
+        if total % e:
+            raise ValueError("source length must be a multiple of elements_to_take_per_leaf")
+        nl = total // e
+        if leafs_sources.dim() == 3 and leafs_sources.shape[2] % e:
+            raise ValueError("each coset must hold whole leaves (merkle_tree.rs:197-198)")
+        if nl <= cap_size:
+            raise ValueError("tree size must exceed cap size (merkle_tree.rs:207)")
+        return cls._chunked(src, c, stride, nl, e, cap_size)
+
+    @classmethod
+    def construct_by_chunking_from_flat_sources(cls, leafs_sources, elements_to_take_per_leaf, cap_size):
+        """merkle_tree.rs:308-386 (FRI intermediate oracles, fri/mod.rs:258-266): as
+        construct_by_chunking over flat (C, N) sources; tree_size == cap_size is allowed (the
+        cap is then the leaf layer)."""
+        src, c, stride, total = _leaf_sources(leafs_sources)
+        e = elements_to_take_per_leaf
+        _log2(e)
+        _log2(cap_size)
+        if total % e:
+            raise ValueError("poly size must be a multiple of elements_to_take_per_leaf")
+        nl = total // e
+        if nl < cap_size:
+            raise ValueError("trying to make tree of size %d with cap %d" % (nl, cap_size))
+        return cls._chunked(src, c, stride, nl, e, cap_size)
+
+    @classmethod
+    def _chunked(cls, src, c, stride, nl, e, cap_size):
+        _log2(nl)
+        dev = src.device
+        leaves = torch.empty((nl, 4), dtype=torch.int64, device=dev)
+        nodes = torch.empty((nl - cap_size, 4), dtype=torch.int64, device=dev)
+        st = stream_of(src)
+        call("bj_merkle_leaves_chunked_d", src.data_ptr(), c, stride, nl, e, leaves.data_ptr(), st)
+        if nl > cap_size:
+            call("bj_merkle_nodes_d", leaves.data_ptr(), nl, cap_size, nodes.data_ptr(), st)
+        return cls(cap_size, leaves, nodes)
+
     @property
     def n_leaves(self):
         return self.leaf_hashes.shape[0]
@@ -117,6 +163,8 @@ class MerkleTreeWithCap:
 
     def get_cap(self):
         """merkle_tree.rs:451-460 -> numpy (cap_size, 4) canonical."""
+        if self.n_leaves == self.cap_size:
+            return to_host(self.leaf_hashes)
         return to_host(self.nodes[-self.cap_size:])
 
     def get_proof(self, idx):

@@ -230,3 +230,58 @@ def sharded_witness_commit(trace_shard, ws, timer=None):
         ops.nodes(ws.roots, ws.cap_size, ws.top_nodes)
         ws.cap.copy_(ws.top_nodes[-ws.cap_size:])
     return ws
+
+
+def _subtree_level(leaves, nodes, n_leaves, level):
+    """Level `level` (0 = leaves) of a tree stored as leaves + concatenated node levels."""
+    if level == 0:
+        return leaves
+    off, ln = 0, n_leaves
+    for _ in range(level - 1):
+        ln //= 2
+        off += ln
+    return nodes[off: off + ln // 2]
+
+
+def sharded_query(ws, tree_idx):
+    """OracleQuery::construct (proof.rs:65-97) for a one-element-per-column leaf over a sharded
+    commit: leaf_elements = every column's LDE value at flat leaf index tree_idx (coset * n +
+    row), proof = MerkleTreeWithCap::get_proof (merkle_tree.rs:462-480) of the global tree.
+    The owning rank reads its row and its subtree path; when cap < G the replicated top levels
+    (gathered roots) finish the path. Collective over ws.group: every rank returns the same
+    (leaf_elements (C,), leaf_hash (4,), proof (depth, 4)) as host int64 tensors."""
+    import torch.distributed as dist
+    nl = ws.m * ws.world
+    if not 0 <= tree_idx < nl:
+        raise ValueError("tree index out of range")
+    owner, local = divmod(tree_idx, ws.m)
+    local_depth = _log2(ws.m) - _log2(ws.cap_local)
+    top_depth = _log2(ws.world) - _log2(ws.cap_size) if ws.cap_size < ws.world else 0
+    size = ws.n_cols + 4 + 4 * (local_depth + top_depth)
+    buf = torch.zeros(size, dtype=torch.int64, device=ws.lde.device)
+    if ws.rank == owner:
+        parts = [ws.lde[:, local], ws.leaves[local]]
+        idx = local
+        for lvl in range(local_depth):
+            parts.append(_subtree_level(ws.leaves, ws.nodes, ws.m, lvl)[idx ^ 1])
+            idx >>= 1
+        buf.copy_(torch.cat([p.reshape(-1) for p in parts] + [torch.zeros(4 * top_depth, dtype=torch.int64,
+                                                                          device=buf.device)]))
+    if top_depth:
+        # the top tree over the G subtree roots is replicated on every rank
+        idx = owner
+        tops = []
+        for lvl in range(top_depth):
+            tops.append(_subtree_level(ws.roots, ws.top_nodes, ws.world, lvl)[idx ^ 1])
+            idx >>= 1
+        buf[size - 4 * top_depth:] = torch.cat([t.reshape(-1) for t in tops])
+    if ws.world > 1:
+        if dist.get_backend(ws.group) == "nccl":
+            dist.broadcast(buf, src=owner, group=ws.group)
+        else:
+            host = buf.cpu()
+            dist.broadcast(host, src=owner, group=ws.group)
+            buf = host
+    buf = buf.cpu()
+    c = ws.n_cols
+    return buf[:c], buf[c:c + 4], buf[c + 4:].reshape(-1, 4)

@@ -21,6 +21,8 @@ hipError_t launch_leaves(const uint64_t* src, size_t col_stride, uint32_t n_cols
                          hipStream_t st);
 hipError_t launch_leaves_partial(const uint64_t* src, size_t col_stride, uint32_t n_cols, size_t n_leaves,
                                  const uint64_t* cap_in, uint64_t* out, bool final_, hipStream_t st);
+hipError_t launch_leaves_chunked(const uint64_t* src, size_t col_stride, uint32_t n_cols, uint32_t log_e,
+                                 size_t n_leaves, uint64_t* out, hipStream_t st);
 hipError_t launch_nodes(const uint64_t* leaves, size_t n_leaves, uint32_t cap_size, uint64_t* nodes,
                         hipStream_t st);
 hipError_t launch_permute(uint64_t* states, size_t count, hipStream_t st);

@@ -480,6 +480,16 @@ int bj_merkle_leaves_partial_d(const uint64_t* src, uint32_t n_cols, size_t col_
     return BJ_OK;
 }
 
+int bj_merkle_leaves_chunked_d(const uint64_t* src, uint32_t n_cols, size_t col_stride, size_t n_leaves,
+                               uint32_t elems_per_leaf, uint64_t* out, void* stream) {
+    if (!is_pow2(elems_per_leaf)) return fail(BJ_EINVAL, "elements_to_take_per_leaf must be a power of two");
+    uint32_t log_e = 0;
+    while ((1u << log_e) < elems_per_leaf) log_e++;
+    if ((uint64_t)n_cols << log_e > 0xFFFFFFFFull) return fail(BJ_EINVAL, "leaf too long");
+    HIP_TRY(bj::launch_leaves_chunked(src, col_stride, n_cols, log_e, n_leaves, out, S(stream)), "leaves");
+    return BJ_OK;
+}
+
 int bj_merkle_nodes_d(const uint64_t* leaves, size_t n_leaves, uint32_t cap_size, uint64_t* nodes, void* stream) {
     if (!is_pow2(n_leaves) || !is_pow2(cap_size) || n_leaves <= cap_size)
         return fail(BJ_EINVAL, "need power-of-two n_leaves > cap_size (merkle_tree.rs:83-96)");

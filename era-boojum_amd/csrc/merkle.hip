@@ -98,6 +98,47 @@ __global__ __launch_bounds__(LEAF_THREADS) void leaf_hash_kernel(const uint64_t*
     else store_canon4_at(s, 2, out + 4 * L);
 }
 
+// Leaf hashing of MerkleTreeWithCap::construct_by_chunking (merkle_tree.rs:176-306) and
+// construct_by_chunking_from_flat_sources (:308-386): leaf L absorbs, for each source column
+// c in order, the E = 2^log_e consecutive elements src[c][L*E .. (L+1)*E).  Used by the FRI
+// oracles (fri/mod.rs:179-187, 258-266: c0 and c1 of the Ext2 codeword, E = 2^r).  One leaf
+// per lane; element k of the leaf's sequence is (c = k >> log_e, t = k & (E-1)).
+__global__ __launch_bounds__(LEAF_THREADS) void leaf_chunk_kernel(const uint64_t* __restrict__ src,
+                                                                  size_t col_stride, uint32_t n_cols,
+                                                                  uint32_t log_e, size_t n_leaves,
+                                                                  uint64_t* __restrict__ out) {
+    const size_t L = blockIdx.x * (size_t)LEAF_THREADS + threadIdx.x;
+    if (L >= n_leaves) return;
+    const uint32_t E = 1u << log_e;
+    const uint64_t* p = src + (L << log_e);
+    p2::State s;
+#pragma unroll
+    for (int i = 0; i < 12; i++) s.lo[i] = s.hi[i] = 0;
+    const uint32_t total = n_cols << log_e;
+    uint32_t k = 0;
+    for (; k + 8 <= total; k += 8) {
+#pragma unroll
+        for (int i = 0; i < 8; i++) {
+            const uint32_t e = k + i;
+            const uint64_t v = p[(size_t)(e >> log_e) * col_stride + (e & (E - 1))];
+            s.lo[i] = (uint32_t)v;
+            s.hi[i] = (uint32_t)(v >> 32);
+        }
+        p2::permute(s);
+    }
+    if (k < total) {
+#pragma unroll
+        for (int i = 0; i < 8; i++) {
+            const uint32_t e = k + i;
+            const uint64_t v = e < total ? p[(size_t)(e >> log_e) * col_stride + (e & (E - 1))] : 0;
+            s.lo[i] = (uint32_t)v;
+            s.hi[i] = (uint32_t)(v >> 32);
+        }
+        p2::permute(s);
+    }
+    store_canon4(s, out + 4 * L);
+}
+
 __device__ __forceinline__ void node_hash(const uint64_t* l, const uint64_t* r, uint64_t* o) {
     p2::State s;
 #pragma unroll
@@ -187,6 +228,14 @@ hipError_t launch_leaves_partial(const uint64_t* src, size_t col_stride, uint32_
         else BJ_LEAF(false, false);
     }
 #undef BJ_LEAF
+    return hipGetLastError();
+}
+
+hipError_t launch_leaves_chunked(const uint64_t* src, size_t col_stride, uint32_t n_cols, uint32_t log_e,
+                                 size_t n_leaves, uint64_t* out, hipStream_t st) {
+    if (n_leaves == 0) return hipSuccess;
+    hipLaunchKernelGGL(leaf_chunk_kernel, dim3((unsigned)((n_leaves + LEAF_THREADS - 1) / LEAF_THREADS)),
+                       dim3(LEAF_THREADS), 0, st, src, col_stride, n_cols, log_e, n_leaves, out);
     return hipGetLastError();
 }
 

@@ -144,6 +144,15 @@ int bj_hash_into_node_h(const uint64_t* left4, const uint64_t* right4, uint64_t*
 int bj_merkle_leaves_d(const uint64_t* src, uint32_t n_cols, size_t col_stride, size_t n_leaves,
                        uint64_t* leaves, void* stream);
 
+/* Leaf hashing of MerkleTreeWithCap::construct_by_chunking (merkle_tree.rs:176-306) and
+ * construct_by_chunking_from_flat_sources (:308-386), the FRI oracles' trees (fri/mod.rs:179-187,
+ * 258-266): leaf L = hash_into_leaf of, for each column c in order, the elems_per_leaf
+ * consecutive elements src[c * col_stride + L * elems_per_leaf + t].  elems_per_leaf is a power
+ * of two.  With a [c][coset][row] LDE the flat leaf index runs over the cosets in order, as the
+ * reference's per-coset chunks do.  leaves: n_leaves x 4. */
+int bj_merkle_leaves_chunked_d(const uint64_t* src, uint32_t n_cols, size_t col_stride, size_t n_leaves,
+                               uint32_t elems_per_leaf, uint64_t* out, void* stream);
+
 /* Leaf hashing over a column range, continuing a sponge (the column-pipelined multi-GPU
  * commit absorbs column chunks as they arrive).  The Overwrite sponge replaces the rate words
  * with each 8-element group, so between groups its whole carried state is the capacity

@@ -187,6 +187,19 @@ def merkle_construct(lde_flat, cap_size, threads=1):
     return leaves, nodes[:n_nodes], levels, cap
 
 
+def merkle_construct_by_chunking(sources_flat, elements_per_leaf, cap_size, threads=1):
+    """MerkleTreeWithCap::construct_by_chunking / construct_by_chunking_from_flat_sources
+    (merkle_tree.rs:176-386): leaf L hashes, for each source c in order, the E consecutive
+    elements sources[c][L*E .. (L+1)*E).  Restated as an ordinary tree over C*E rows, row
+    c*E + t holding sources[c][L*E + t] for leaf L."""
+    src = _u64(sources_flat)
+    c, total = src.shape
+    e = elements_per_leaf
+    nl = total // e
+    rows = np.ascontiguousarray(src.reshape(c, nl, e).transpose(0, 2, 1).reshape(c * e, nl))
+    return merkle_construct(rows, cap_size, threads=threads)
+
+
 def merkle_get_proof(leaves, nodes, levels, idx):
     nl = leaves.shape[0]
     leaf = np.zeros(4, dtype=np.uint64)

@@ -1,5 +1,6 @@
 #!/bin/bash
-# rocprofv3 evidence for the C3 bench: kernel-trace stats, then one PMC pass per counter group.
+# rocprofv3 evidence for the C3 bench: the default bench line (with the CPU baseline), a
+# kernel-trace stats run, then one PMC pass per counter group.
 # usage: bash scripts/profile_r1.sh TAG
 set -u
 TAG=${1:-r1}
@@ -7,6 +8,8 @@ cd "$GRAFT_REPO_ROOT"
 export TMPDIR=/tmp
 OUT=gpurun_out/prof_$TAG
 mkdir -p $OUT
+timeout -k 10 400 python3 bench.py > $OUT/bench_default.log 2>&1 || { echo "bench rc=$?"; tail -5 $OUT/bench_default.log; exit 1; }
+tail -1 $OUT/bench_default.log
 B="python3 bench.py --config C3 --no-cpu-baseline"
 timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d $OUT/trace -o run -- $B --steps 3 --warmup 1 > $OUT/trace.log 2>&1 || { echo "trace rc=$?"; tail -5 $OUT/trace.log; exit 1; }
 echo trace ok
@@ -16,4 +19,3 @@ timeout -s KILL 240 rocprofv3 --pmc WRITE_SIZE --output-format csv -d $OUT/write
 echo write ok
 timeout -s KILL 240 rocprofv3 --pmc SQ_INSTS_VALU SQ_WAVES SQ_BUSY_CYCLES SQ_WAVE_CYCLES SQ_ACTIVE_INST_VALU GRBM_GUI_ACTIVE --output-format csv -d $OUT/sq -o run -- $B --steps 1 --warmup 0 > $OUT/sq.log 2>&1 || { echo "sq rc=$?"; tail -5 $OUT/sq.log; exit 1; }
 echo sq ok
-find $OUT -name "*.csv" | head -20

@@ -32,7 +32,12 @@ def run(rank, world, port, cfg, outdir, device, paths):
         if dev != "cpu":
             torch.cuda.synchronize()
         u = lambda t: t.cpu().numpy().view(np.uint64)  # noqa: E731
+        from boojum_amd.sharded import sharded_query
+        nl = ws.m * world
+        qidx = sorted({0, nl - 1, nl // 3, ws.m, (5 * nl) // 7})
+        qs = [sharded_query(ws, i) for i in qidx]
         np.savez(os.path.join(outdir, "rank%d.npz" % rank), lde=u(ws.lde), leaves=u(ws.leaves), nodes=u(ws.nodes),
-                 cap=u(ws.cap))
+                 cap=u(ws.cap), qidx=np.array(qidx), q_elems=np.stack([u(q[0]) for q in qs]),
+                 q_leaf=np.stack([u(q[1]) for q in qs]), q_path=np.stack([u(q[2]) for q in qs]))
     finally:
         dist.destroy_process_group()

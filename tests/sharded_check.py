@@ -49,3 +49,12 @@ def run_and_check(world, cfg, tmp_path, device):
             lo += cnt
             k += 1
         assert lo == r["nodes"].shape[0]
+        # openings (OracleQuery::construct): identical on every rank, equal to the full tree's
+        levels = (nl.bit_length() - 1) - (cap.bit_length() - 1)
+        for j, idx in enumerate(r["qidx"]):
+            idx = int(idx)
+            leaf, path = O.merkle_get_proof(ref["leaves"], ref["nodes"], levels, idx)
+            assert np.array_equal(r["q_elems"][j], lde_flat[:, idx]), "rank %d query %d elements" % (P, idx)
+            assert np.array_equal(r["q_leaf"][j], leaf), "rank %d query %d leaf" % (P, idx)
+            assert np.array_equal(r["q_path"][j], path), "rank %d query %d path" % (P, idx)
+            assert O.verify_proof_over_cap(r["q_path"][j], ref["cap"], r["q_leaf"][j], idx)

@@ -251,6 +251,56 @@ def test_leaves_partial_rejects_ragged_middle(bj):
         call("bj_merkle_leaves_partial_d", None, 7, 1, 1, None, None, 0, None)
 
 
+@pytest.mark.parametrize("c,total,e,cap", [(2, 1 << 12, 8, 32), (2, 1 << 10, 16, 1), (3, 1 << 9, 1, 4), (1, 64, 2, 8),
+                                           (2, 256, 8, 32), (5, 1 << 11, 4, 16)])
+def test_construct_by_chunking_flat(bj, c, total, e, cap):
+    """FRI oracles' trees (fri/mod.rs:179-187, 258-266), incl. tree_size == cap_size."""
+    src = rand((c, total), c * 31 + e)
+    t = bj.field.to_device(src)
+    T = bj.merkle.MerkleTreeWithCap
+    nl = total // e
+    tree = T.construct_by_chunking_from_flat_sources(t, e, cap)
+    leaves, nodes, levels, capr = O.merkle_construct_by_chunking(src, e, cap, threads=4)
+    eq(bj.field.to_host(tree.leaf_hashes), leaves)
+    eq(tree.get_cap(), capr)
+    if nl > cap:
+        eq(bj.field.to_host(tree.nodes), nodes)
+        tree2 = T.construct_by_chunking(t, e, cap)
+        eq(tree2.get_cap(), capr)
+        leaf, path = tree.get_proof(nl - 1)
+        assert T.verify_proof_over_cap(path, tree.get_cap(), leaf, nl - 1)
+
+
+def test_construct_by_chunking_over_lde_cosets(bj):
+    """construct_by_chunking over a (C, D, n) LDE: the flat leaf index runs over the cosets."""
+    x = rand((2, 1 << 10), 55)
+    t = bj.field.to_device(x)
+    l = bj.lde.transform_raw_storages_to_lde(t, 4)
+    tree = bj.merkle.MerkleTreeWithCap.construct_by_chunking(l, 8, 16)
+    _, l_ref = O.lde(x, 2)
+    leaves, nodes, levels, capr = O.merkle_construct_by_chunking(l_ref.reshape(2, -1), 8, 16)
+    eq(bj.field.to_host(tree.leaf_hashes), leaves)
+    eq(tree.get_cap(), capr)
+
+
+def test_fri_base_oracle_leaves_from_fixture_on_gpu(bj):
+    """The proof.json FRI base-oracle leaves (8 elements of c0 then 8 of c1) hashed by the
+    chunked leaf kernel verify against the committed FRI cap."""
+    import json
+    import os
+    from boojum_amd._lib import call
+    fx = json.load(open(os.path.join(os.path.dirname(__file__), "golden", "proof_queries.json")))
+    T = bj.merkle.MerkleTreeWithCap
+    for q in fx["queries"]:
+        f = q["fri_base"]
+        el = np.array(f["leaf_elements"], dtype=np.uint64).reshape(2, 8)   # sources c0, c1
+        t = bj.field.to_device(el)
+        out = bj.torch.empty((1, 4), dtype=bj.torch.int64, device=t.device)
+        call("bj_merkle_leaves_chunked_d", t.data_ptr(), 2, 8, 1, 8, out.data_ptr(), bj.field.stream_of(t))
+        leaf = bj.field.to_host(out)[0]
+        assert T.verify_proof_over_cap(f["proof"], fx["caps"]["fri_base"], leaf, f["index"])
+
+
 # --------------------------------------------------------------- commit
 
 @pytest.mark.parametrize("c,log_n,log_d,cap", [(32, 16, 1, 16), (7, 10, 2, 8), (9, 9, 3, 16), (1, 4, 1, 2)])

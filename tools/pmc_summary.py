@@ -10,8 +10,9 @@ Units and gfx950 corrections (MI355X_MICROARCH.md, HBM section):
 * FETCH_SIZE reports half the bytes of a wide contiguous stream. That holds for the leaf kernel and the NTT tails
   (512 contiguous bytes per wave load; leaf: FETCH_SIZE = 16 GiB against its known 32 GiB of reads;
   tails: the inverse + forward average 10.1 GiB against a known 20 GiB).
-  The NTT heads read 128-byte runs, and their FETCH_SIZE equals their known byte count
-  (iNTT head: 8 GiB), so they are not doubled.
+  The NTT heads read 128-byte runs. The DIF heads' FETCH_SIZE equalled their known byte count
+  (iNTT head: 8 GiB), so they are not doubled; the CT heads (other grid order) report half of
+  it (iNTT head: 4.3 GB against 8 GiB), so they are.
 The per-kernel factor is the third field of KERNELS; each was calibrated on a known byte count.
 
 usage: python tools/pmc_summary.py gpurun_out/prof_TAG [--config C3]
@@ -24,21 +25,23 @@ import os
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 
-# kernel-name prefix -> (key, FETCH_SIZE read factor)
+# kernel-name prefix (after an optional "void ") -> (key, FETCH_SIZE read factor)
 KERNELS = [
     ("bj::leaf_hash_kernel", "leaf_hash_kernel", 2.0),
     ("bj::node_level_kernel", "node_level_kernel", 1.0),
     ("bj::node_tail_kernel", "node_tail_kernel", 1.0),
-    ("void bj::(anonymous namespace)::ct_head_kernel<9, 1", "ct_head_fwd", 1.0),
-    ("void bj::(anonymous namespace)::ct_head_kernel<9, 0", "ct_head_inv", 1.0),
+    ("bj::(anonymous namespace)::ct_head_kernel<9, 1", "ct_head_fwd", 2.0),
+    ("bj::(anonymous namespace)::ct_head_kernel<9, 0", "ct_head_inv", 2.0),
     ("bj::(anonymous namespace)::ct_tail_kernel", "ct_tail", 2.0),
-    ("void bj::(anonymous namespace)::dif_head_kernel<9, 1>", "dif_head_fwd", 1.0),
-    ("void bj::(anonymous namespace)::dif_head_kernel<9, 0>", "dif_head_inv", 1.0),
+    ("bj::(anonymous namespace)::dif_head_kernel<9, 1>", "dif_head_fwd", 1.0),
+    ("bj::(anonymous namespace)::dif_head_kernel<9, 0>", "dif_head_inv", 1.0),
     ("bj::(anonymous namespace)::dif_tail_kernel", "dif_tail", 2.0),
 ]
 
 
 def key_of(name):
+    if name.startswith("void "):
+        name = name[5:]
     for pre, key, fac in KERNELS:
         if name.startswith(pre):
             return key, fac
