@@ -45,28 +45,22 @@ __device__ __forceinline__ void split2(uint64_t x, uint32_t& lo, uint32_t& hi) {
 }
 __device__ __forceinline__ uint64_t join2(uint32_t lo, uint32_t hi) { return ((uint64_t)hi << 32) | lo; }
 
-// CT butterflies on four pairs: t = c * mu; (a, c) <- (a + t, a - t).
+// CT butterflies on four pairs: t = c * mu; (a, c) <- (a + t, a - t) in place
+// (glasm::ct_bfly_x4: t canonicalised, then single-correction subtract and add).
 __device__ __forceinline__ void ct_bfly_x4(uint64_t& xa0, uint64_t& xc0, uint64_t& xa1, uint64_t& xc1,
                                            uint64_t& xa2, uint64_t& xc2, uint64_t& xa3, uint64_t& xc3, uint64_t w0,
                                            uint64_t w1, uint64_t w2, uint64_t w3) {
-    uint32_t c0[4], c1[4], v0[4], v1[4], t0[4], t1[4];
-    split2(xc0, c0[0], c1[0]); split2(w0, v0[0], v1[0]);
-    split2(xc1, c0[1], c1[1]); split2(w1, v0[1], v1[1]);
-    split2(xc2, c0[2], c1[2]); split2(w2, v0[2], v1[2]);
-    split2(xc3, c0[3], c1[3]); split2(w3, v0[3], v1[3]);
-    glasm::mul_x4(c0[0], c1[0], v0[0], v1[0], t0[0], t1[0], c0[1], c1[1], v0[1], v1[1], t0[1], t1[1],
-                  c0[2], c1[2], v0[2], v1[2], t0[2], t1[2], c0[3], c1[3], v0[3], v1[3], t0[3], t1[3]);
-    uint32_t a0[4], a1[4], s0[4], s1[4], d0[4], d1[4];
-    split2(xa0, a0[0], a1[0]); split2(xa1, a0[1], a1[1]);
-    split2(xa2, a0[2], a1[2]); split2(xa3, a0[3], a1[3]);
-    glasm::add_x4(a0[0], a1[0], t0[0], t1[0], s0[0], s1[0], a0[1], a1[1], t0[1], t1[1], s0[1], s1[1],
-                  a0[2], a1[2], t0[2], t1[2], s0[2], s1[2], a0[3], a1[3], t0[3], t1[3], s0[3], s1[3]);
-    glasm::sub_x4(a0[0], a1[0], t0[0], t1[0], d0[0], d1[0], a0[1], a1[1], t0[1], t1[1], d0[1], d1[1],
-                  a0[2], a1[2], t0[2], t1[2], d0[2], d1[2], a0[3], a1[3], t0[3], t1[3], d0[3], d1[3]);
-    xa0 = join2(s0[0], s1[0]); xc0 = join2(d0[0], d1[0]);
-    xa1 = join2(s0[1], s1[1]); xc1 = join2(d0[1], d1[1]);
-    xa2 = join2(s0[2], s1[2]); xc2 = join2(d0[2], d1[2]);
-    xa3 = join2(s0[3], s1[3]); xc3 = join2(d0[3], d1[3]);
+    uint32_t a0[4], a1[4], c0[4], c1[4], v0[4], v1[4];
+    split2(xa0, a0[0], a1[0]); split2(xc0, c0[0], c1[0]); split2(w0, v0[0], v1[0]);
+    split2(xa1, a0[1], a1[1]); split2(xc1, c0[1], c1[1]); split2(w1, v0[1], v1[1]);
+    split2(xa2, a0[2], a1[2]); split2(xc2, c0[2], c1[2]); split2(w2, v0[2], v1[2]);
+    split2(xa3, a0[3], a1[3]); split2(xc3, c0[3], c1[3]); split2(w3, v0[3], v1[3]);
+    glasm::ct_bfly_x4(a0[0], a1[0], c0[0], c1[0], v0[0], v1[0], a0[1], a1[1], c0[1], c1[1], v0[1], v1[1],
+                      a0[2], a1[2], c0[2], c1[2], v0[2], v1[2], a0[3], a1[3], c0[3], c1[3], v0[3], v1[3]);
+    xa0 = join2(a0[0], a1[0]); xc0 = join2(c0[0], c1[0]);
+    xa1 = join2(a0[1], a1[1]); xc1 = join2(c0[1], c1[1]);
+    xa2 = join2(a0[2], a1[2]); xc2 = join2(c0[2], c1[2]);
+    xa3 = join2(a0[3], a1[3]); xc3 = join2(c0[3], c1[3]);
 }
 
 __device__ __forceinline__ void mul4_by(uint64_t& x0, uint64_t& x1, uint64_t& x2, uint64_t& x3, uint64_t k) {

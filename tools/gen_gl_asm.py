@@ -41,7 +41,7 @@ class Stream:
         self.instrs = instrs  # list of (text, reads_sgprs set, writes_sgprs set)
 
 
-def mul_stream(k, vbase):
+def mul_stream(k, vbase, out=None):
     """z = a * b mod p in 14 instructions.  Inputs a0,a1,b0,b1; outputs z0,z1.
     Scratch pairs P,U,W,V at vbase..vbase+7, m at vbase+8; carries cA, cB, cW.
 
@@ -56,6 +56,8 @@ def mul_stream(k, vbase):
     P, U, W, V = ["v[%d:%d]" % (vbase + 2 * i, vbase + 2 * i + 1) for i in range(4)]
     cA, cB, cW = sp(3 * k), sp(3 * k + 1), sp(3 * k + 2)
     a0, a1, b0, b1, z0, z1 = ["%%[%s%d]" % (n, k) for n in ("a0", "a1", "b0", "b1", "z0", "z1")]
+    if out is not None:
+        z0, z1 = out
     I = []
     I.append(("v_mad_u64_u32 %s, %s, %s, %s, 0" % (U, JUNK, a1, b0), set(), {JUNK}))
     I.append(("v_mad_u64_u32 %s, %s, %s, %s, 0" % (P, JUNK, a0, b0), set(), {JUNK}))
@@ -117,6 +119,60 @@ def addsub_stream(k, vbase, op):
             I.append(("v_sub_co_u32 %s, %s, %s, %s" % (z0, cA, z0, M), set(), {cA}))
             I.append(("v_subb_co_u32 %s, %s, %s, 0, %s" % (z1, cA, z1, cA), {cA}, {cA}))
     return I
+
+
+def ct_bfly_stream(k, vbase):
+    """Cooley-Tukey butterfly in place: (a, c) <- (a + c w, a - c w), 28 instructions.
+    t = c * w (mul_stream, result left in its U pair), canonicalised (t + EPS overflows iff
+    t >= p).  With t < p, a - t borrows at most once and a + t wraps 2^64 at most once, so each
+    needs a single EPS correction (5 instructions instead of 8).  The difference goes into c's
+    registers (c is dead after the products), then the sum into a's.
+    Operands: a0,a1 and c0,c1 read-write; w0,w1 read."""
+    P0, P1, U0, U1 = ["v%d" % (vbase + i) for i in range(4)]
+    M = "v%d" % (vbase + 8)
+    p0, p1, p2 = sp(3 * k), sp(3 * k + 1), sp(3 * k + 2)
+    a0, a1, c0, c1 = ["%%[%s%d]" % (n, k) for n in ("a0", "a1", "c0", "c1")]
+    I = []
+    for t, r, w in mul_stream(k, vbase, out=(U0, U1)):
+        t = t.replace("%%[b0%d]" % k, "%%[w0%d]" % k).replace("%%[b1%d]" % k, "%%[w1%d]" % k)
+        t = t.replace("%%[a0%d]" % k, "%%[c0%d]" % k).replace("%%[a1%d]" % k, "%%[c1%d]" % k)
+        I.append((t, r, w))
+    # canonical t: X = t + EPS (into the dead P pair); carry => t >= p => t = X
+    I.append(("v_add_co_u32 %s, %s, %s, -1" % (P0, p0, U0), set(), {p0}))
+    I.append(("v_addc_co_u32 %s, %s, %s, 0, %s" % (P1, p0, U1, p0), {p0}, {p0}))
+    I.append(("v_cndmask_b32_e64 %s, %s, %s, %s" % (U0, U0, P0, p0), {p0}, set()))
+    I.append(("v_cndmask_b32_e64 %s, %s, %s, %s" % (U1, U1, P1, p0), {p0}, set()))
+    # c = a - t: one borrow at most, worth -2^64 == -EPS
+    I.append(("v_sub_co_u32 %s, %s, %s, %s" % (c0, p1, a0, U0), set(), {p1}))
+    I.append(("v_subb_co_u32 %s, %s, %s, %s, %s" % (c1, p1, a1, U1, p1), {p1}, {p1}))
+    I.append(("v_cndmask_b32_e64 %s, 0, -1, %s" % (M, p1), {p1}, set()))
+    I.append(("v_sub_co_u32 %s, %s, %s, %s" % (c0, p2, c0, M), set(), {p2}))
+    I.append(("v_subb_co_u32 %s, %s, %s, 0, %s" % (c1, JUNK, c1, p2), {p2}, {JUNK}))
+    # a = a + t: one wrap at most, worth 2^64 == EPS
+    I.append(("v_add_co_u32 %s, %s, %s, %s" % (a0, p0, a0, U0), set(), {p0}))
+    I.append(("v_addc_co_u32 %s, %s, %s, %s, %s" % (a1, p0, a1, U1, p0), {p0}, {p0}))
+    I.append(("v_cndmask_b32_e64 %s, 0, -1, %s" % (M, p0), {p0}, set()))
+    I.append(("v_add_co_u32 %s, %s, %s, %s" % (a0, p1, a0, M), set(), {p1}))
+    I.append(("v_addc_co_u32 %s, %s, %s, 0, %s" % (a1, JUNK, a1, p1), {p1}, {JUNK}))
+    return I
+
+
+def emit_ct_bfly(n):
+    streams = [ct_bfly_stream(k, 10 * k) for k in range(n)]  # 64-bit tuples even-aligned
+    body = interleave(streams)
+    args, outs, ins = [], [], []
+    for k in range(n):
+        args += ["uint32_t& a0%d" % k, "uint32_t& a1%d" % k, "uint32_t& c0%d" % k, "uint32_t& c1%d" % k,
+                 "uint32_t w0%d" % k, "uint32_t w1%d" % k]
+        outs += ['[%s%d] "+v"(%s%d)' % (nm, k, nm, k) for nm in ("a0", "a1", "c0", "c1")]
+        ins += ['[%s%d] "v"(%s%d)' % (nm, k, nm, k) for nm in ("w0", "w1")]
+    clob = ['"v%d"' % i for i in range(10 * n - 1)] + ['"s%d"' % i for i in range(SGPR_BASE, SGPR_BASE + 26)]
+    lines = ["// %d in-place Cooley-Tukey butterflies (a, c) <- (a + c w, a - c w) (28 instructions each)" % n,
+             "__device__ __forceinline__ void ct_bfly_x%d(%s) {" % (n, ", ".join(args)), "    asm volatile("]
+    lines += ['        "%s\\n"' % t for t in body]
+    lines += ["        : %s" % ", ".join(outs), "        : %s" % ", ".join(ins), "        : %s);" % ", ".join(clob),
+              "}"]
+    return "\n".join(lines) + "\n"
 
 
 def canon_stream(k, vbase):
@@ -290,6 +346,8 @@ namespace glasm {
                              ["a0", "a1", "b0", "b1"], ["z0", "z1"], doc="%d general additions" % n))
         parts.append(emit_fn("sub_x%d" % n, n, lambda k, vb: addsub_stream(k, vb, "sub"), 2,
                              ["a0", "a1", "b0", "b1"], ["z0", "z1"], doc="%d general subtractions" % n))
+    for n in (1, 4):
+        parts.append(emit_ct_bfly(n))
     for n in (1, 2, 4):
         parts.append(emit_fn("canon_x%d" % n, n, canon_stream, 2, ["a0", "a1"], ["z0", "z1"],
                              doc="%d canonicalisations z = x mod p in [0, p)" % n))
