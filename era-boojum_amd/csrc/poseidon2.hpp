@@ -129,15 +129,24 @@ __device__ __forceinline__ void full_round(State& s, uint64_t* L, uint64_t* H, i
     mds_ext_limbs(s.hi, H);
 }
 
-// One partial round on a reduced state: s0 += RC, s0 = s0^7, then M_I.
-__device__ __forceinline__ void partial_round(State& s, int r) {
-    {
-        uint64_t L0 = (uint64_t)s.lo[0] + RCL.lo[r][0];
-        uint64_t H0 = (uint64_t)s.hi[0] + RCL.hi[r][0];
-        glasm::reduce_x1(L0, (uint32_t)H0, (uint32_t)(H0 >> 32), s.lo[0], s.hi[0]);
-        sbox_x1(s.lo[0], s.hi[0]);
-    }
-    glasm::mi_layer(s.lo, s.hi);
+// Partial-round S-box on a reduced s0: s0 += RC_r, s0 = s0^7.
+__device__ __forceinline__ void partial_sbox(State& s, int r) {
+    uint64_t L0 = (uint64_t)s.lo[0] + RCL.lo[r][0];
+    uint64_t H0 = (uint64_t)s.hi[0] + RCL.hi[r][0];
+    glasm::reduce_x1(L0, (uint32_t)H0, (uint32_t)(H0 >> 32), s.lo[0], s.hi[0]);
+    sbox_x1(s.lo[0], s.hi[0]);
+}
+
+// Two partial rounds r, r + 1.  M_I of round r leaves elements 1..11 as unreduced limbs
+// (< 2^46.6); only s0, the next S-box input, is reduced.  Round r + 1's M_I consumes the limbs
+// (sums < 2^50.2, shifted terms < 2^61) and reduces every element.  Same field values as two
+// reduced rounds (glasm::mi_layer_a / mi_layer_b, tools/gen_gl_asm.py).
+__device__ __forceinline__ void partial_round_pair(State& s, int r) {
+    uint64_t L[12], H[12];
+    partial_sbox(s, r);
+    glasm::mi_layer_a(s.lo, s.hi, L, H);
+    partial_sbox(s, r + 1);
+    glasm::mi_layer_b(s.lo, s.hi, L, H);
 }
 
 // The permutation (state_generic_impl.rs:221-236): MDS; 4 x (RC, S-box, MDS);
@@ -150,7 +159,7 @@ __device__ __forceinline__ void permute(State& s) {
     for (int r = 0; r < 4; r++) full_round(s, L, H, r);
     reduce12(L, H, s.lo, s.hi);
 #pragma unroll 1
-    for (int r = 4; r < 26; r++) partial_round(s, r);
+    for (int r = 4; r < 26; r += 2) partial_round_pair(s, r);
 #pragma unroll
     for (int i = 0; i < 12; i++) {
         L[i] = s.lo[i];

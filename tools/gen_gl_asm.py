@@ -324,6 +324,142 @@ def emit_mi_layer():
     return "\n".join(lines) + "\n"
 
 
+# v_lshl_add_u64 shift amounts verified on gfx950 hardware (tools/isa_probe.hip)
+MAX_LSHL_ADD_SHIFT = 4
+
+
+def reduce_limbs(Lp, Hp, Wp, M, c, z0, z1):
+    """The 5-instruction limb reduction (reduce_stream) on register pairs Lp, Hp -> z0, z1."""
+    H0, H1 = Hp.split("[")[1].rstrip("]").split(":")
+    H0, H1 = "v" + H0, "v" + H1
+    W0, W1 = Wp.split("[")[1].rstrip("]").split(":")
+    W0, W1 = "v" + W0, "v" + W1
+    return [
+        ("v_mad_u64_u32 %s, %s, %s, -1, %s" % (Wp, JUNK, H1, Lp), set(), {JUNK}),
+        ("v_add_co_u32 %s, %s, %s, %s" % (W1, c, W1, H0), set(), {c}),
+        ("v_cndmask_b32_e64 %s, 0, -1, %s" % (M, c), {c}, set()),
+        ("v_add_co_u32 %s, %s, %s, %s" % (z0, c, W0, M), set(), {c}),
+        ("v_addc_co_u32 %s, %s, %s, 0, %s" % (z1, JUNK, W1, c), {c}, {JUNK}),
+    ]
+
+
+def _consts(pro):
+    consts = {}
+    sreg = SGPR_BASE + 26
+    for k in sorted(set(SH)):
+        if k > 6:
+            consts[k] = "s%d" % sreg
+            pro.append(("s_mov_b32 s%d, %d" % (sreg, 1 << k), set(), set()))
+            sreg += 1
+    return consts, sreg
+
+
+def emit_mi_layer_a():
+    """First partial round of a pair: M_I with elements 1..11 left as unreduced limbs.
+    L_i = lo_i 2^SH[i] + sum lo_j, H_i likewise (one mad each, < 2^46.6); only element 0,
+    the next S-box input, is reduced.  The pair's second round (mi_layer_b) reduces all."""
+    pro = []
+    consts, sreg = _consts(pro)
+    SUM = {("L", c): "v[%d:%d]" % (2 * c, 2 * c + 1) for c in range(3)}
+    SUM.update({("H", c): "v[%d:%d]" % (6 + 2 * c, 7 + 2 * c) for c in range(3)})
+    chains = []
+    for limb, src in (("L", "lo"), ("H", "hi")):
+        for c in range(3):
+            ch = []
+            for t in range(4):
+                i = 4 * c + t
+                acc = SUM[(limb, c)]
+                ch.append(("v_mad_u64_u32 %s, %s, %%[%s%d], 1, %s" % (acc, JUNK, src, i, "0" if t == 0 else acc),
+                           set(), {JUNK}))
+            chains.append(ch)
+    body = pro + merge(chains)
+    for limb in ("L", "H"):
+        a = SUM[(limb, 0)]
+        body.append(("v_lshl_add_u64 %s, %s, 0, %s" % (a, SUM[(limb, 1)], a), set(), set()))
+        body.append(("v_lshl_add_u64 %s, %s, 0, %s" % (a, SUM[(limb, 2)], a), set(), set()))
+    Ls, Hs = SUM[("L", 0)], SUM[("H", 0)]
+    for i in range(1, 12):
+        K = consts.get(SH[i], str(1 << SH[i]))
+        body.append(("v_mad_u64_u32 %%[L%d], %s, %%[lo%d], %s, %s" % (i, JUNK, i, K, Ls), set(), {JUNK}))
+        body.append(("v_mad_u64_u32 %%[H%d], %s, %%[hi%d], %s, %s" % (i, JUNK, i, K, Hs), set(), {JUNK}))
+    body.append(("v_mad_u64_u32 v[12:13], %s, %%[lo0], %d, %s" % (JUNK, 1 << SH[0], Ls), set(), {JUNK}))
+    body.append(("v_mad_u64_u32 v[14:15], %s, %%[hi0], %d, %s" % (JUNK, 1 << SH[0], Hs), set(), {JUNK}))
+    body += reduce_limbs("v[12:13]", "v[14:15]", "v[16:17]", "v18", sp(0), "%[lo0]", "%[hi0]")
+    text = pad(body)
+    args = "uint32_t* lo, uint32_t* hi, uint64_t* L, uint64_t* H"
+    outs = ['[lo0] "+v"(lo[0])', '[hi0] "+v"(hi[0])']
+    outs += ['[L%d] "=&v"(L[%d]), [H%d] "=&v"(H[%d])' % (i, i, i, i) for i in range(1, 12)]
+    ins = ['[lo%d] "v"(lo[%d]), [hi%d] "v"(hi[%d])' % (i, i, i, i) for i in range(1, 12)]
+    clob = ['"v%d"' % i for i in range(20)] + ['"s%d"' % i for i in range(SGPR_BASE, sreg)]
+    n_v = sum(1 for t in text if t.startswith("v_"))
+    lines = ["// Poseidon2 partial round M_I, first of a pair: elements 1..11 as limbs L, H (%d VALU instructions)" % n_v,
+             "__device__ __forceinline__ void mi_layer_a(%s) {" % args, "    asm volatile("]
+    lines += ['        "%s\\n"' % t for t in text]
+    lines += ["        : %s" % ", ".join(outs), "        : %s" % ", ".join(ins), "        : %s);" % ", ".join(clob), "}"]
+    return "\n".join(lines) + "\n"
+
+
+def emit_mi_layer_b():
+    """Second partial round of a pair: M_I on element 0 (reduced lo0, hi0) and elements 1..11
+    as the limbs L_i, H_i < 2^46.6 left by mi_layer_a.  Sums over limbs < 2^50.2;
+    L_i' = L_i << SH[i] + sum < 2^61 (one v_lshl_add_u64 when SH[i] <= MAX_LSHL_ADD_SHIFT,
+    else shift + add); then the 5-instruction reduction of every element."""
+    pro = []
+    consts, sreg = _consts(pro)
+    Ls, Hs = "v[0:1]", "v[2:3]"
+    Ls2, Hs2 = "v[4:5]", "v[6:7]"
+    body = list(pro)
+    # two chains per limb for ILP: (0, 1..5) and (6..11)
+    chains = []
+    for acc, acc2, src, lim in ((Ls, Ls2, "lo", "L"), (Hs, Hs2, "hi", "H")):
+        ch = [("v_mad_u64_u32 %s, %s, %%[%s0], 1, %%[%s1]" % (acc, JUNK, src, lim), set(), {JUNK})]
+        for j in range(2, 6):
+            ch.append(("v_lshl_add_u64 %s, %%[%s%d], 0, %s" % (acc, lim, j, acc), set(), set()))
+        ch2 = [("v_lshl_add_u64 %s, %%[%s6], 0, %%[%s7]" % (acc2, lim, lim), set(), set())]
+        for j in range(8, 12):
+            ch2.append(("v_lshl_add_u64 %s, %%[%s%d], 0, %s" % (acc2, lim, j, acc2), set(), set()))
+        chains += [ch, ch2]
+    body += merge(chains)
+    body.append(("v_lshl_add_u64 %s, %s, 0, %s" % (Ls, Ls2, Ls), set(), set()))
+    body.append(("v_lshl_add_u64 %s, %s, 0, %s" % (Hs, Hs2, Hs), set(), set()))
+    for g in range(3):
+        streams = []
+        for j in range(4):
+            i = 4 * g + j
+            base = 8 + 8 * j
+            Lp = "v[%d:%d]" % (base, base + 1)
+            Hp = "v[%d:%d]" % (base + 2, base + 3)
+            Wp = "v[%d:%d]" % (base + 4, base + 5)
+            M = "v%d" % (base + 6)
+            c = sp(j)
+            st = []
+            if i == 0:
+                st.append(("v_mad_u64_u32 %s, %s, %%[lo0], %d, %s" % (Lp, JUNK, 1 << SH[0], Ls), set(), {JUNK}))
+                st.append(("v_mad_u64_u32 %s, %s, %%[hi0], %d, %s" % (Hp, JUNK, 1 << SH[0], Hs), set(), {JUNK}))
+            else:
+                for P, lim, S in ((Lp, "L", Ls), (Hp, "H", Hs)):
+                    if SH[i] <= MAX_LSHL_ADD_SHIFT:
+                        st.append(("v_lshl_add_u64 %s, %%[%s%d], %d, %s" % (P, lim, i, SH[i], S), set(), set()))
+                    else:
+                        st.append(("v_lshlrev_b64 %s, %d, %%[%s%d]" % (P, SH[i], lim, i), set(), set()))
+                        st.append(("v_lshl_add_u64 %s, %s, 0, %s" % (P, P, S), set(), set()))
+            st += reduce_limbs(Lp, Hp, Wp, M, c, "%%[lo%d]" % i, "%%[hi%d]" % i)
+            streams.append(st)
+        body += merge(streams)
+    text = pad(body)
+    args = "uint32_t* lo, uint32_t* hi, const uint64_t* L, const uint64_t* H"
+    outs = ['[lo0] "+v"(lo[0])', '[hi0] "+v"(hi[0])']
+    outs += ['[lo%d] "=&v"(lo[%d]), [hi%d] "=&v"(hi[%d])' % (i, i, i, i) for i in range(1, 12)]
+    ins = ['[L%d] "v"(L[%d]), [H%d] "v"(H[%d])' % (i, i, i, i) for i in range(1, 12)]
+    clob = ['"v%d"' % i for i in range(8 + 32)] + ['"s%d"' % i for i in range(SGPR_BASE, sreg)]
+    n_v = sum(1 for t in text if t.startswith("v_"))
+    lines = ["// Poseidon2 partial round M_I, second of a pair: reduces every element (%d VALU instructions)" % n_v,
+             "__device__ __forceinline__ void mi_layer_b(%s) {" % args, "    asm volatile("]
+    lines += ['        "%s\\n"' % t for t in text]
+    lines += ["        : %s" % ", ".join(outs), "        : %s" % ", ".join(ins), "        : %s);" % ", ".join(clob), "}"]
+    return "\n".join(lines) + "\n"
+
+
 def main():
     parts = ['''// GENERATED by tools/gen_gl_asm.py -- do not edit.
 // gfx950 inline-asm Goldilocks primitives (see the generator's docstring for the
@@ -352,6 +488,8 @@ namespace glasm {
         parts.append(emit_fn("canon_x%d" % n, n, canon_stream, 2, ["a0", "a1"], ["z0", "z1"],
                              doc="%d canonicalisations z = x mod p in [0, p)" % n))
     parts.append(emit_mi_layer())
+    parts.append(emit_mi_layer_a())
+    parts.append(emit_mi_layer_b())
     parts.append("}  // namespace glasm\n")
     with open(OUT, "w") as f:
         f.write("\n".join(parts))

@@ -2,10 +2,10 @@
 """Static VALU census of one Poseidon2 permutation as compiled for gfx950.
 
 The permutation (csrc/poseidon2.hpp) has three `#pragma unroll 1` round loops with fixed
-trip counts: 4 full rounds, 22 partial rounds and 4 full rounds. `node_level_kernel`
+trip counts: 4 full rounds, 11 pairs of partial rounds and 4 full rounds. `node_level_kernel`
 (csrc/merkle.hip) runs exactly one permutation per lane, so its dynamic instruction
 stream is known statically:
-    straight-line code x1 + loop bodies x (4, 22, 4).
+    straight-line code x1 + loop bodies x (4, 11, 4).
 This tool disassembles the gfx950 code object and weights each VALU instruction by the
 issue cost measured in profiles/r1_isa_rates.txt:
 * 1 slot: full-rate 32-bit ops (v_add_u32, v_mov_b32, logic);
@@ -70,7 +70,7 @@ def parse(lines):
     return instrs
 
 
-def census(instrs, trips=(4, 22, 4)):
+def census(instrs, trips=(4, 11, 4)):
     base = instrs[0][0]
     back = [(i, a, t) for i, (a, mn, t) in enumerate(instrs) if t is not None and base + t < a]
     if len(back) != len(trips):
