@@ -38,7 +38,7 @@ import torch
 from ._lib import call
 from .field import stream_of
 
-CHUNK_TARGET_COLS = 64   # columns per pipelined all-gather chunk (at least 8 G)
+CHUNK_TARGET_COLS = 32   # columns per pipelined all-gather chunk (at least 8 G): a small first chunk exposes little exchange
 
 
 def _log2(n):
