@@ -43,6 +43,7 @@ SIGNATURES = {
     "bj_merkle_nodes_d": ([_vp, _sz, _u32, _vp, _vp], _int),
     "bj_lde_commit_d": ([_vp, _u32, _sz, _u32, _u32, _u32, _vp, _vp, _vp, _vp, _u64p, _vp], _int),
     "bj_lde_commit_h": ([_u64p, _u32, _u32, _u32, _u32, _u64p, _u64p, _u64p, _u64p], _int),
+    "bj_fri_fold_d": ([_vp, _vp, _sz, _vp, _u64, _u64, _u64, _vp, _vp, _vp], _int),
     "bj_fill_synthetic_d": ([_vp, _u32, _sz, _u32, _u64, _u64, _vp], _int),
     "bj_gl_op_d": ([_int, _vp, _vp, _vp, _sz, _vp], _int),
 }

@@ -68,3 +68,10 @@ hipError_t launch_ct(uint64_t* dst, size_t dst_col_stride, size_t coset_stride, 
                      const uint64_t* tab, size_t tab_stride, uint64_t kappa, bool canon_out, hipStream_t st);
 hipError_t launch_scale(uint64_t* cols, size_t stride, uint32_t n_cols, size_t n, uint64_t k, hipStream_t st);
 }  // namespace bj
+
+namespace bj {
+// fri.hip: one FRI fold by 2 of a GoldilocksExt2 codeword (c0, c1)
+hipError_t launch_fri_fold(const uint64_t* c0, const uint64_t* c1, size_t n_out, const uint64_t* roots,
+                           uint64_t coset_inverse, uint64_t ch0, uint64_t ch1, uint64_t* d0, uint64_t* d1,
+                           hipStream_t st);
+}  // namespace bj

@@ -445,6 +445,15 @@ int bj_lde_shard_d(const uint64_t* coeffs, uint32_t n_cols, size_t coeffs_stride
     return BJ_OK;
 }
 
+int bj_fri_fold_d(const uint64_t* c0, const uint64_t* c1, size_t n_src, const uint64_t* roots,
+                  uint64_t coset_inverse, uint64_t ch0, uint64_t ch1, uint64_t* dst_c0, uint64_t* dst_c1,
+                  void* stream) {
+    if (n_src < 2 || (n_src & 1)) return fail(BJ_EINVAL, "a fold needs an even source length >= 2");
+    HIP_TRY(bj::launch_fri_fold(c0, c1, n_src / 2, roots, coset_inverse, ch0, ch1, dst_c0, dst_c1, S(stream)),
+            "fri fold");
+    return BJ_OK;
+}
+
 int bj_fill_synthetic_d(uint64_t* dst, uint32_t n_cols, size_t col_stride, uint32_t log_n, uint64_t seed,
                         uint64_t first_col, void* stream) {
     if (int r = check_log_n(log_n)) return r;

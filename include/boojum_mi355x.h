@@ -190,6 +190,19 @@ int bj_lde_commit_h(const uint64_t* trace_h, uint32_t n_cols, uint32_t log_n, ui
                     uint32_t cap_size, uint64_t* lde_h, uint64_t* leaves_h, uint64_t* nodes_h,
                     uint64_t* cap_h);
 
+/* ------------------------------------------------------------------- FRI */
+
+/* One FRI fold by 2 of a GoldilocksExt2 codeword stored as base columns c0, c1 of n_src
+ * bit-reversed values (fold_multiple, cs/implementations/fri/mod.rs:362-474, as driven by
+ * interpolate_independent_cosets :476-585 and interpolate_flattened_cosets :587-682):
+ *   dst_i = f(x) + f(-x) + alpha * (f(x) - f(-x)) * roots[i] * coset_inverse,  i < n_src / 2,
+ * f(x) = (c0[2i], c1[2i]), f(-x) = (c0[2i+1], c1[2i+1]), alpha = (ch0, ch1), u^2 = 7.
+ * roots: the INVERSED bit-reversed twiddles of the full FRI domain (bj_precompute_twiddles_d
+ * with inverse = 1), indexed by the flat pair index.  Device pointers; outputs canonical. */
+int bj_fri_fold_d(const uint64_t* c0, const uint64_t* c1, size_t n_src, const uint64_t* roots,
+                  uint64_t coset_inverse, uint64_t ch0, uint64_t ch1, uint64_t* dst_c0, uint64_t* dst_c1,
+                  void* stream);
+
 /* ------------------------------------------------------------- utility */
 
 /* Batched field arithmetic through the device field layer (utility for parity tests of

@@ -278,3 +278,23 @@ def naive_coset_lde_column(col, log_d):
             acc = (acc * x + c) % P
         out.append(acc)
     return out
+
+
+def fri_fold(c0, c1, roots, coset_inverse, challenge):
+    """fold_multiple (cs/implementations/fri/mod.rs:362-474) in Python ints (test sizes only):
+    out_i = f(x) + f(-x) + alpha * (f(x) - f(-x)) * roots[i] * coset_inverse over GoldilocksExt2
+    (u^2 = 7, field/traits/field.rs:407-424), f(x) at 2i, f(-x) at 2i + 1."""
+    ch0, ch1 = int(challenge[0]) % P, int(challenge[1]) % P
+    n = len(c0) // 2
+    d0 = np.zeros(n, dtype=np.uint64)
+    d1 = np.zeros(n, dtype=np.uint64)
+    for i in range(n):
+        x0, mx0, x1, mx1 = int(c0[2 * i]), int(c0[2 * i + 1]), int(c1[2 * i]), int(c1[2 * i + 1])
+        r = int(roots[i]) * coset_inverse % P
+        a0 = (x0 - mx0) * r % P
+        a1 = (x1 - mx1) * r % P
+        e0 = (a0 * ch0 + 7 * a1 * ch1) % P
+        e1 = (a0 * ch1 + a1 * ch0) % P
+        d0[i] = (e0 + x0 + mx0) % P
+        d1[i] = (e1 + x1 + mx1) % P
+    return d0, d1
