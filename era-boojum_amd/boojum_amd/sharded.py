@@ -194,13 +194,14 @@ def sharded_witness_commit(trace_shard, ws, timer=None):
     if tuple(trace_shard.shape) != (ws.cols_per_rank, 1 << ws.log_n):
         raise ValueError("trace shard must be (%d, %d)" % (ws.cols_per_rank, 1 << ws.log_n))
     runs = ws.column_runs()
-    timer.start("ifft")
-    for lo, g, c in runs:
-        ops.coeffs(trace_shard[lo:lo + c], ws.coeffs[g:g + c], ws.log_n)
-    timer.stop("ifft")
     K = ws.chunk_cols
     handles = []
+    # chunk k's all-gather is issued as soon as this rank's part of it is transformed, so it
+    # overlaps the transforms of the later chunks
     for k, (lo, g, c) in enumerate(runs):
+        timer.start("ifft")
+        ops.coeffs(trace_shard[lo:lo + c], ws.coeffs[g:g + c], ws.log_n)
+        timer.stop("ifft")
         if ws.world > 1:
             handles.append(_all_gather(ws.coeffs[k * K:(k + 1) * K], ws.coeffs[g:g + c], ws.group, async_op=True))
         else:
