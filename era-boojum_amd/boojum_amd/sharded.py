@@ -20,13 +20,14 @@ pool). This is its multi-GPU split (BASELINE north_star):
 Column pipeline (C a multiple of 8 G). The leaf sponge absorbs columns in order, 8 per
 permutation, and between 8-column groups its only carried state is the 4 capacity words
 (bj_merkle_leaves_partial_d). So the columns are dealt to ranks in 8-column blocks, and the
-exchange runs as one all-gather per chunk of b blocks per rank (8 b G consecutive columns).
-All chunks' all-gathers are issued up front on RCCL's stream. Chunk k's coset transform and
-sponge absorption then run on the compute stream as soon as chunk k has arrived, while later
-chunks are still on the wire. Block ownership: global 8-column block k*b*G + P*b + j
-(chunk k, j < b) belongs to rank P, at local block k*b + j. Otherwise (C not a multiple of
-8 G) rank P holds the contiguous columns [P*C/G, (P+1)*C/G) and one all-gather runs
-before the transforms.
+exchange runs as one all-gather per chunk of b_k blocks per rank (8 b_k G consecutive
+columns; b = 1, 1, 2, 4, 4, ...). Each chunk's all-gather is issued on RCCL's stream as soon
+as this rank's part of it is inverse-transformed. Chunk k's coset transform and sponge
+absorption then run on the compute stream as soon as chunk k has arrived, while later chunks
+are still on the wire. Block ownership: global 8-column block B_k*G + P*b_k + j (chunk k,
+j < b_k, B_k = b_0 + ... + b_{k-1}) belongs to rank P, at local block B_k + j. Otherwise
+(C not a multiple of 8 G) rank P holds the contiguous columns [P*C/G, (P+1)*C/G) and one
+all-gather runs before the transforms.
 
 Outputs stay sharded: each rank keeps its LDE slice, its leaves and subtree nodes, and
 the full cap. The compute steps are an `ops` object: `HipShardOps` (the C ABI on the
@@ -38,7 +39,21 @@ import torch
 from ._lib import call
 from .field import stream_of
 
-CHUNK_TARGET_COLS = 32   # columns per pipelined all-gather chunk (at least 8 G): a small first chunk exposes little exchange
+MAX_CHUNK_BLOCKS = 4   # largest pipelined chunk, in 8-column blocks per rank
+
+
+def _chunk_schedule(blocks_per_rank, max_blocks=MAX_CHUNK_BLOCKS):
+    """Blocks per rank in each pipelined chunk: 1, 1, 2, 4, ... capped at max_blocks.  The first
+    chunks are small so little of the exchange is exposed before the pipeline fills; later
+    ones are larger so the per-chunk launch and tail costs stay small."""
+    sched, done, b = [], 0, 1
+    while done < blocks_per_rank:
+        take = min(b, blocks_per_rank - done)
+        sched.append(take)
+        done += take
+        if len(sched) >= 2:
+            b = min(2 * b, max_blocks)
+    return sched
 
 
 def _log2(n):
@@ -111,7 +126,7 @@ class ShardedWorkspace:
     """
 
     def __init__(self, n_cols, log_n, log_lde, cap_size, rank, world, device="cuda", group=None, ops=None,
-                 chunk_cols=CHUNK_TARGET_COLS):
+                 max_chunk_blocks=MAX_CHUNK_BLOCKS):
         log_g = _log2(world)
         _log2(cap_size)
         if n_cols % world:
@@ -134,15 +149,11 @@ class ShardedWorkspace:
         # column pipeline geometry
         self.pipelined = n_cols % (8 * world) == 0
         if self.pipelined:
-            blocks_per_rank = n_cols // (8 * world)
-            b = max(1, chunk_cols // (8 * world))
-            while blocks_per_rank % b:
-                b -= 1
-            self.b = b
-            self.n_chunks = blocks_per_rank // b
-            self.chunk_cols = 8 * b * world
+            self.schedule = _chunk_schedule(n_cols // (8 * world), max_chunk_blocks)
         else:
-            self.b, self.n_chunks, self.chunk_cols = None, 1, n_cols
+            self.schedule = [None]
+        self.n_chunks = len(self.schedule)
+        self.chunk_cols = n_cols if not self.pipelined else 8 * world * max(self.schedule)
         kw = dict(dtype=torch.int64, device=device)
         self.coeffs = torch.empty((n_cols, n), **kw)
         self.work = torch.empty((self.chunk_cols, m), **kw) if log_g > log_lde else None
@@ -160,12 +171,24 @@ class ShardedWorkspace:
             call("bj_prepare", log_n)
 
     def column_runs(self):
-        """This rank's columns as (local_first, global_first, count) runs, in local order."""
+        """This rank's columns as (local_first, global_first, count) runs, one per chunk, in
+        local order.  Chunk k (b_k blocks per rank) covers global columns
+        [8 G B_k, 8 G (B_k + b_k)), B_k = sum of the earlier b; rank P owns its P-th 8 b_k slice."""
         P = self.rank
         if not self.pipelined:
             return [(0, P * self.cols_per_rank, self.cols_per_rank)]
-        run = 8 * self.b
-        return [(k * run, k * self.chunk_cols + P * run, run) for k in range(self.n_chunks)]
+        runs, B = [], 0
+        for b in self.schedule:
+            runs.append((8 * B, 8 * (B * self.world + P * b), 8 * b))
+            B += b
+        return runs
+
+    def chunk_columns(self, k):
+        """Global column range [lo, hi) of chunk k."""
+        if not self.pipelined:
+            return 0, self.n_cols
+        B = sum(self.schedule[:k])
+        return 8 * self.world * B, 8 * self.world * (B + self.schedule[k])
 
     @property
     def my_columns(self):
@@ -194,7 +217,6 @@ def sharded_witness_commit(trace_shard, ws, timer=None):
     if tuple(trace_shard.shape) != (ws.cols_per_rank, 1 << ws.log_n):
         raise ValueError("trace shard must be (%d, %d)" % (ws.cols_per_rank, 1 << ws.log_n))
     runs = ws.column_runs()
-    K = ws.chunk_cols
     handles = []
     # chunk k's all-gather is issued as soon as this rank's part of it is transformed, so it
     # overlaps the transforms of the later chunks
@@ -203,13 +225,15 @@ def sharded_witness_commit(trace_shard, ws, timer=None):
         ops.coeffs(trace_shard[lo:lo + c], ws.coeffs[g:g + c], ws.log_n)
         timer.stop("ifft")
         if ws.world > 1:
-            handles.append(_all_gather(ws.coeffs[k * K:(k + 1) * K], ws.coeffs[g:g + c], ws.group, async_op=True))
+            c0, c1 = ws.chunk_columns(k)
+            handles.append(_all_gather(ws.coeffs[c0:c1], ws.coeffs[g:g + c], ws.group, async_op=True))
         else:
             handles.append(_Done())
     for k in range(ws.n_chunks):
         handles[k].wait()
-        cols = slice(k * K, (k + 1) * K)
-        work = None if ws.work is None else ws.work[:K]
+        c0, c1 = ws.chunk_columns(k)
+        cols = slice(c0, c1)
+        work = None if ws.work is None else ws.work[:c1 - c0]
         timer.start("lde")
         ops.lde_shard(ws.coeffs[cols], ws.log_n, ws.log_lde, ws.log_g, ws.rank, work, ws.lde[cols])
         timer.stop("lde")

@@ -54,8 +54,8 @@ def test_lde_shard_errors(torch_mod):
         call("bj_lde_shard_d", None, 1, 16, 4, 1, 2, 1, None, None, None)   # G > D without work
 
 
-@pytest.mark.parametrize("world,cfg", [(2, (8, 10, 1, 16)), (4, (8, 9, 1, 2)), (2, (48, 10, 2, 16, 16)),
-                                       (4, (64, 12, 1, 4, 32)), (8, (64, 9, 1, 16))])
+@pytest.mark.parametrize("world,cfg", [(2, (8, 10, 1, 16)), (4, (8, 9, 1, 2)), (2, (48, 10, 2, 16, 1)),
+                                       (4, (64, 12, 1, 4, 1)), (8, (64, 9, 1, 16)), (2, (256, 9, 1, 16))])
 def test_sharded_commit_multirank_one_gpu(torch_mod, world, cfg, tmp_path):
     from sharded_check import run_and_check
     run_and_check(world, cfg, tmp_path, "cuda")

@@ -14,9 +14,10 @@ from sharded_check import run_and_check
     (2, (2, 4, 2, 2)),    # G < D
     (4, (4, 4, 1, 2)),    # G > D (sub-cosets), cap < G
     (4, (8, 5, 2, 16)),   # G == D, cap > G
-    (2, (32, 5, 1, 4, 16)),   # column pipeline: 2 chunks of 16 columns, G == D
-    (4, (64, 4, 1, 2, 32)),   # column pipeline: 2 chunks, G > D (sub-cosets), cap < G
-    (2, (48, 4, 2, 8, 16)),   # column pipeline: 3 chunks, G < D
+    (2, (32, 5, 1, 4, 1)),    # column pipeline: 2 chunks of 16 columns, G == D
+    (4, (64, 4, 1, 2, 1)),    # column pipeline: 2 chunks, G > D (sub-cosets), cap < G
+    (2, (48, 4, 2, 8, 1)),    # column pipeline: 3 chunks, G < D
+    (2, (128, 4, 1, 4)),      # column pipeline: chunks of 1, 1, 2, 4 blocks per rank
 ])
 def test_sharded_commit_gloo(world, cfg, tmp_path):
     run_and_check(world, cfg, tmp_path, "cpu")
