@@ -135,11 +135,16 @@ __device__ __forceinline__ void head_b_stage(uint64_t* x, const uint64_t* __rest
 // MODE 0: natural source; MODE 1: bit-reversed source gathered in runs of 2^R words.
 // KAPPA: multiply the stage-0 lower operands by kappa (the inverse table's CT[1] already
 // carries it for the upper ones), i.e. scale the whole transform by kappa.
+// Grid: one dimension, XCD-aware.  Blocks are dealt round-robin over the 8 XCDs, so the
+// n_cosets blocks of one (column, tile) unit sit at ids unit8 + 8 c within a run of 8 n_cosets
+// ids: they share an XCD (its L2) and run at about the same time, so the source tile is
+// fetched from HBM once and re-read from L2 by the other cosets (speed only; any placement
+// gives the same result).
 template <int R, int MODE, bool KAPPA>
 __global__ __launch_bounds__(NT, 2) void ct_head_kernel(uint64_t* dst, size_t dst_col_stride, size_t coset_stride,
                                                         const uint64_t* src, size_t src_stride, uint32_t log_n,
                                                         const uint64_t* __restrict__ tab, size_t tab_stride,
-                                                        uint64_t kappa) {
+                                                        uint64_t kappa, uint32_t n_cosets, uint32_t log_tiles) {
     constexpr int LOGW = 13 - R;
     constexpr uint32_t W = 1u << LOGW;
     constexpr uint32_t T = 1u << (R - 5);
@@ -147,9 +152,14 @@ __global__ __launch_bounds__(NT, 2) void ct_head_kernel(uint64_t* dst, size_t ds
     const uint32_t tid = threadIdx.x;
     const size_t n = (size_t)1 << log_n;
     const size_t S = n >> R;
-    const size_t o0 = (size_t)blockIdx.y * W;
-    const uint64_t* sc = src + (size_t)blockIdx.x * src_stride;
-    const uint64_t* ct = tab + (size_t)blockIdx.z * tab_stride;
+    const uint32_t bid = blockIdx.x;
+    const uint32_t rest = bid >> 3;
+    const uint32_t coset = rest % n_cosets;
+    const uint32_t unit = ((rest / n_cosets) << 3) | (bid & 7);
+    const uint32_t col = unit >> log_tiles;
+    const size_t o0 = (size_t)(unit & ((1u << log_tiles) - 1)) * W;
+    const uint64_t* sc = src + (size_t)col * src_stride;
+    const uint64_t* ct = tab + (size_t)coset * tab_stride;
     const uint32_t w = tid & (W - 1);
     const uint32_t s = tid >> LOGW;
     const size_t o = o0 + w;
@@ -193,7 +203,7 @@ __global__ __launch_bounds__(NT, 2) void ct_head_kernel(uint64_t* dst, size_t ds
 #pragma unroll
     for (int k = 0; k < PT; k++) x[k] = lds[swz_head<LOGW>((32 * s + k) * W + w)];
     head_b_stage<R, 5>(x, ct, s);
-    uint64_t* dc = dst + (size_t)blockIdx.x * dst_col_stride + (size_t)blockIdx.z * coset_stride;
+    uint64_t* dc = dst + (size_t)col * dst_col_stride + (size_t)coset * coset_stride;
 #pragma unroll
     for (int k = 0; k < PT; k++) dc[(size_t)(32 * s + k) * S + o] = x[k];
 }
@@ -326,9 +336,11 @@ template <int R>
 void launch_head_R(int mode, bool kappa_on, dim3 g, uint64_t* dst, size_t dst_col_stride, size_t coset_stride,
                    const uint64_t* src, size_t src_stride, uint32_t log_n, const uint64_t* tab, size_t tab_stride,
                    uint64_t kappa, hipStream_t st) {
-#define BJ_CT_HEAD(M, K)                                                                                        \
-    hipLaunchKernelGGL((ct_head_kernel<R, M, K>), g, dim3(NT), 0, st, dst, dst_col_stride, coset_stride, src, \
-                       src_stride, log_n, tab, tab_stride, kappa)
+    const uint32_t log_tiles = log_n - 13;
+    const dim3 g1(g.x * g.y * g.z);
+#define BJ_CT_HEAD(M, K)                                                                                         \
+    hipLaunchKernelGGL((ct_head_kernel<R, M, K>), g1, dim3(NT), 0, st, dst, dst_col_stride, coset_stride, src, \
+                       src_stride, log_n, tab, tab_stride, kappa, g.z, log_tiles)
     if (mode == 0) {
         if (kappa_on) BJ_CT_HEAD(0, true);
         else BJ_CT_HEAD(0, false);
