@@ -2,8 +2,9 @@
 
 * C2 (2^20 x 128, LDE x2, cap 16): bit-exact against the CPU oracle end to end (LDE,
   leaves, nodes, cap). This is BASELINE.json configs[1] "bit-exact vs CPU LDE + caps".
-* C3 (2^22 x 256, LDE x4, cap 16, the bench workload): the oracle would need minutes, so
-  the checks are size-independent properties of the same commit:
+* C3 (2^22 x 256, LDE x4, cap 16, the bench workload) and C4 (2^23 x 256, LDE x8, the 8-GPU
+  sizing case, 164 GB of HBM on one GPU): the oracle would need minutes, so the checks are
+  size-independent properties of the same commit:
   - three whole columns (first, middle, last) equal the oracle's LDE of those columns;
   - 256 sampled leaves are re-hashed on the CPU from the GPU's LDE rows;
   - every node level is spot-checked: sampled parents re-hashed from their two children;
@@ -53,11 +54,13 @@ def test_c2_bit_exact(bj):
     eq(bj.field.to_host(ws.lde), ref["lde"], "lde")
 
 
-def test_c3_properties(bj):
+@pytest.mark.parametrize("cfg", [(256, 22, 2, 16), (256, 23, 3, 16)], ids=["C3", "C4"])
+def test_fullsize_properties(bj, cfg):
     torch = bj.torch
-    c, log_n, log_d, cap = 256, 22, 2, 16
+    c, log_n, log_d, cap = cfg
     n, D = 1 << log_n, 1 << log_d
     nl = n * D
+    torch.cuda.empty_cache()
     tr = bj.commit.synthetic_trace(c, log_n)
     ws = bj.commit.witness_commit(tr, D, cap)
     torch.cuda.synchronize()
