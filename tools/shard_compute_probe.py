@@ -1,0 +1,61 @@
+#!/usr/bin/env python3
+"""Per-rank compute of the G-way sharded commit, measured on one GPU with the exchange
+stubbed out: rank P's LDE range, leaves and subtree for G = 1, 2, 4, 8 at C3.  The result
+bounds the multi-GPU step time from below (exchange fully hidden).  It is not a bench
+line (the coefficient buffer holds this rank's own columns only, so the values are not a
+real commit).
+
+usage: python tools/shard_compute_probe.py [config]
+"""
+import json
+import os
+import sys
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, os.path.join(ROOT, "era-boojum_amd"))
+sys.path.insert(0, ROOT)
+
+
+def main():
+    import torch
+    import bench
+    from boojum_amd import sharded
+    cfg = sys.argv[1] if len(sys.argv) > 1 else "C3"
+    n_cols, log_n, log_lde, cap = bench.CONFIGS[cfg]
+    out = {}
+
+    def compute(ws, tr):
+        """sharded_witness_commit without its collectives (rank 0's compute only)."""
+        ops = ws.ops
+        for k, (lo, g, c) in enumerate(ws.column_runs()):
+            ops.coeffs(tr[lo:lo + c], ws.coeffs[g:g + c], ws.log_n)
+        for k in range(ws.n_chunks):
+            c0, c1 = ws.chunk_columns(k)
+            work = None if ws.work is None else ws.work[:c1 - c0]
+            ops.lde_shard(ws.coeffs[c0:c1], ws.log_n, ws.log_lde, ws.log_g, ws.rank, work, ws.lde[c0:c1])
+            last = k == ws.n_chunks - 1
+            ops.leaves(ws.lde[c0:c1], ws.leaves if last else ws.state, cap_in=None if k == 0 else ws.state,
+                       final=last)
+        ops.nodes(ws.leaves, ws.cap_local, ws.nodes)
+
+    for world in (1, 2, 4, 8):
+        ws = sharded.ShardedWorkspace(n_cols, log_n, log_lde, cap, 0, world, device="cuda")
+        tr = ws.synthetic_trace_shard()
+        compute(ws, tr)   # warm-up
+        torch.cuda.synchronize()
+        s, e = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        s.record()
+        for _ in range(3):
+            compute(ws, tr)
+        e.record()
+        torch.cuda.synchronize()
+        ms = s.elapsed_time(e) / 3
+        out[world] = {"ms_per_rank": round(ms, 2), "chunks": ws.n_chunks,
+                      "ideal_elems_per_s": n_cols * (1 << log_n) / (ms * 1e-3)}
+        del ws, tr
+        torch.cuda.empty_cache()
+    print(json.dumps({"config": cfg, "per_rank_compute": out}))
+
+
+if __name__ == "__main__":
+    main()
