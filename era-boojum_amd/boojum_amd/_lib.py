@@ -33,6 +33,8 @@ SIGNATURES = {
     "bj_monomials_to_lde_d": ([_vp, _u32, _sz, _u32, _u32, _vp, _vp], _int),
     "bj_lde_coeffs_d": ([_vp, _u32, _sz, _u32, _vp, _sz, _vp], _int),
     "bj_lde_shard_d": ([_vp, _u32, _sz, _u32, _u32, _u32, _u32, _vp, _vp, _vp], _int),
+    "bj_lde_fold_shards_d": ([_vp, _u32, _sz, _u32, _u32, _u32, _vp, _sz, _vp], _int),
+    "bj_lde_shard_folded_d": ([_vp, _u32, _sz, _u32, _u32, _u32, _u32, _vp, _vp], _int),
     "bj_poseidon2_permute_d": ([_vp, _sz, _vp], _int),
     "bj_poseidon2_permute_h": ([_u64p], _int),
     "bj_hash_into_leaf_h": ([_u64p, _sz, _u64p], _int),

@@ -7,11 +7,15 @@ pool). This is its multi-GPU split (BASELINE north_star):
   * each rank inverse-transforms its own columns into the exchange format
     (bj_lde_coeffs_d: monomials in bit-reversed order), straight into its slice of the
     all-columns coefficient buffer;
-  * all-gathers (RCCL, in place) give every rank every column's coefficients
-    (8 n C bytes in total). They are the only data-path exchange;
-  * rank P evaluates its contiguous range of m = n*D/G leaves of the flat leaf domain
-    (coset * n + row, merkle_tree.rs:112-157): whole cosets when G <= D, a folded sub-coset
-    when G > D (bj_lde_shard_d);
+  * G <= D: all-gathers (RCCL, in place) give every rank every column's coefficients
+    (8 n C bytes in total); rank P evaluates its whole cosets (bj_lde_shard_d);
+  * G > D: rank P's m = n*D/G leaves are a sub-coset, whose evaluation only needs every column
+    folded mod Y^m - s_P^m (m values instead of n). The sender folds its own columns for every
+    rank at once (bj_lde_fold_shards_d) and one all-to-all per chunk delivers them
+    (8 m C bytes in total, G/D times less than the all-gather); rank P transforms what it
+    received (bj_lde_shard_folded_d). These collectives are the only data-path exchange;
+  * rank P's range of the flat leaf domain (coset * n + row, merkle_tree.rs:112-157) is
+    [P m, (P+1) m);
   * leaves and the subtree over them are hashed locally. Contiguous aligned leaf ranges are
     subtrees of the reference's tree, so every node is the reference's node;
   * the cap is all-gathered: cap/G digests per rank when cap >= G. Otherwise every rank
@@ -69,6 +73,15 @@ class HipShardOps:
         call("bj_lde_coeffs_d", trace.data_ptr(), trace.shape[0], trace.stride(0), log_n, out.data_ptr(),
              out.stride(0), stream_of(out))
 
+    def fold_shards(self, coeffs, log_n, log_lde, log_shards, out):
+        g, c, m = out.shape
+        call("bj_lde_fold_shards_d", coeffs.data_ptr(), coeffs.shape[0], coeffs.stride(0), log_n, log_lde, log_shards,
+             out.data_ptr(), out.stride(0), stream_of(out))
+
+    def lde_shard_folded(self, folded, log_n, log_lde, log_shards, shard, lde):
+        call("bj_lde_shard_folded_d", folded.data_ptr(), folded.shape[0], folded.stride(0), log_n, log_lde,
+             log_shards, shard, lde.data_ptr(), stream_of(lde))
+
     def lde_shard(self, coeffs, log_n, log_lde, log_shards, shard, work, lde):
         call("bj_lde_shard_d", coeffs.data_ptr(), coeffs.shape[0], coeffs.stride(0), log_n, log_lde, log_shards,
              shard, None if work is None else work.data_ptr(), lde.data_ptr(), stream_of(lde))
@@ -107,6 +120,20 @@ def _all_gather(out, inp, group=None, async_op=False):
     return _Done() if async_op else None
 
 
+def _all_to_all(out, inp, group=None, async_op=False):
+    """out (G*k, ...) <- block r of out is block `rank` of rank r's inp (G*k, ...). RCCL runs it on
+    device memory (async handle as in _all_gather); gloo stages through the host."""
+    import torch.distributed as dist
+    if dist.get_backend(group) == "nccl":
+        w = dist.all_to_all_single(out, inp, group=group, async_op=async_op)
+        return w if async_op else None
+    src = inp.detach().cpu().contiguous()
+    dst = torch.empty_like(src)
+    dist.all_to_all_single(dst, src, group=group)
+    out.copy_(dst.to(out.device))
+    return _Done() if async_op else None
+
+
 class _NoTimer:
     def start(self, name):
         pass
@@ -118,15 +145,20 @@ class _NoTimer:
 class ShardedWorkspace:
     """Per-rank HBM buffers of a G-way sharded commit of C x 2^log_n at LDE 2^log_lde.
 
+    G <= D (or fold_exchange False):
     coeffs (C, n)             all columns' coefficients (this rank's slices written locally)
     work   (K, m) | None      fold scratch, K = columns per chunk (G > D only)
+    G > D with fold_exchange (the default):
+    own    (C/G, n)           this rank's coefficients
+    send   (C/G * G * m)      its columns folded for every rank, (G, c_k, m) per chunk
+    folded (C, m)             every column folded for this rank (the all-to-all output)
     lde    (C, m)             this rank's leaf range of every column's LDE, m = n*D/G
     state  (m, 4) | None      carried sponge capacity between column chunks
     leaves (m, 4), nodes (m - cap_local, 4), cap (cap, 4)
     """
 
     def __init__(self, n_cols, log_n, log_lde, cap_size, rank, world, device="cuda", group=None, ops=None,
-                 max_chunk_blocks=MAX_CHUNK_BLOCKS):
+                 max_chunk_blocks=MAX_CHUNK_BLOCKS, fold_exchange=True):
         log_g = _log2(world)
         _log2(cap_size)
         if n_cols % world:
@@ -155,8 +187,16 @@ class ShardedWorkspace:
         self.n_chunks = len(self.schedule)
         self.chunk_cols = n_cols if not self.pipelined else 8 * world * max(self.schedule)
         kw = dict(dtype=torch.int64, device=device)
-        self.coeffs = torch.empty((n_cols, n), **kw)
-        self.work = torch.empty((self.chunk_cols, m), **kw) if log_g > log_lde else None
+        self.fold_exchange = bool(fold_exchange) and log_g > log_lde
+        if self.fold_exchange:
+            self.coeffs = self.work = None
+            self.own = torch.empty((self.cols_per_rank, n), **kw)
+            self.send = torch.empty((self.cols_per_rank * world * m,), **kw)
+            self.folded = torch.empty((n_cols, m), **kw)
+        else:
+            self.own = self.send = self.folded = None
+            self.coeffs = torch.empty((n_cols, n), **kw)
+            self.work = torch.empty((self.chunk_cols, m), **kw) if log_g > log_lde else None
         self.lde = torch.empty((n_cols, m), **kw)
         self.state = torch.empty((m, 4), **kw) if self.n_chunks > 1 else None
         self.leaves = torch.empty((m, 4), **kw)
@@ -167,7 +207,7 @@ class ShardedWorkspace:
             self.top_nodes = torch.empty((world - cap_size, 4), **kw)
         if hasattr(self.ops, "prepare"):
             self.ops.prepare(log_n)
-        elif self.coeffs.is_cuda:
+        elif self.lde.is_cuda:
             call("bj_prepare", log_n)
 
     def column_runs(self):
@@ -190,6 +230,11 @@ class ShardedWorkspace:
         B = sum(self.schedule[:k])
         return 8 * self.world * B, 8 * self.world * (B + self.schedule[k])
 
+    def send_chunk(self, lo, c):
+        """(G, c, m) view of the send buffer for the run of c local columns starting at lo."""
+        base = self.world * self.m * lo
+        return self.send[base: base + self.world * c * self.m].view(self.world, c, self.m)
+
     @property
     def my_columns(self):
         return [g + i for _, g, c in self.column_runs() for i in range(c)]
@@ -200,7 +245,7 @@ class ShardedWorkspace:
 
     def synthetic_trace_shard(self):
         """This rank's columns of the synthetic trace, generated in place."""
-        t = torch.empty((self.cols_per_rank, 1 << self.log_n), dtype=torch.int64, device=self.coeffs.device)
+        t = torch.empty((self.cols_per_rank, 1 << self.log_n), dtype=torch.int64, device=self.lde.device)
         for lo, g, c in self.column_runs():
             self.ops.synthetic(t[lo:lo + c], self.log_n, g)
         return t
@@ -221,11 +266,21 @@ def sharded_witness_commit(trace_shard, ws, timer=None):
     # chunk k's all-gather is issued as soon as this rank's part of it is transformed, so it
     # overlaps the transforms of the later chunks
     for k, (lo, g, c) in enumerate(runs):
+        c0, c1 = ws.chunk_columns(k)
+        if ws.fold_exchange:
+            # fold this rank's chunk columns for every rank, then one all-to-all
+            send = ws.send_chunk(lo, c)
+            timer.start("ifft")
+            ops.coeffs(trace_shard[lo:lo + c], ws.own[lo:lo + c], ws.log_n)
+            ops.fold_shards(ws.own[lo:lo + c], ws.log_n, ws.log_lde, ws.log_g, send)
+            timer.stop("ifft")
+            # (fold_exchange implies G > D >= 2)
+            handles.append(_all_to_all(ws.folded[c0:c1], send.view(ws.world * c, ws.m), ws.group, async_op=True))
+            continue
         timer.start("ifft")
         ops.coeffs(trace_shard[lo:lo + c], ws.coeffs[g:g + c], ws.log_n)
         timer.stop("ifft")
         if ws.world > 1:
-            c0, c1 = ws.chunk_columns(k)
             handles.append(_all_gather(ws.coeffs[c0:c1], ws.coeffs[g:g + c], ws.group, async_op=True))
         else:
             handles.append(_Done())
@@ -233,9 +288,12 @@ def sharded_witness_commit(trace_shard, ws, timer=None):
         handles[k].wait()
         c0, c1 = ws.chunk_columns(k)
         cols = slice(c0, c1)
-        work = None if ws.work is None else ws.work[:c1 - c0]
         timer.start("lde")
-        ops.lde_shard(ws.coeffs[cols], ws.log_n, ws.log_lde, ws.log_g, ws.rank, work, ws.lde[cols])
+        if ws.fold_exchange:
+            ops.lde_shard_folded(ws.folded[cols], ws.log_n, ws.log_lde, ws.log_g, ws.rank, ws.lde[cols])
+        else:
+            work = None if ws.work is None else ws.work[:c1 - c0]
+            ops.lde_shard(ws.coeffs[cols], ws.log_n, ws.log_lde, ws.log_g, ws.rank, work, ws.lde[cols])
         timer.stop("lde")
         last = k == ws.n_chunks - 1
         timer.start("leaves")

@@ -48,6 +48,11 @@ namespace bj {
 constexpr uint32_t kMaxFold = 64;
 hipError_t launch_fold(uint64_t* dst, size_t dst_stride, const uint64_t* src, size_t src_stride, uint32_t n_cols,
                        uint32_t log_m, uint32_t log_f, uint64_t s_pow_m, hipStream_t st);
+// the same fold for `shards` targets at once: dst + P * dst_shard_stride + c * dst_col_stride
+// receives column c folded with s_pow_m[P]
+hipError_t launch_fold_all(uint64_t* dst, size_t dst_col_stride, size_t dst_shard_stride, const uint64_t* src,
+                           size_t src_stride, uint32_t n_cols, uint32_t log_m, uint32_t log_f, uint32_t shards,
+                           const uint64_t* s_pow_m, hipStream_t st);
 
 // ntt_fast.hip: register-resident passes for 2^18 <= n <= 2^23
 bool fast_ntt_supported(uint32_t log_n);

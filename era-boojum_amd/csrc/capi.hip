@@ -286,6 +286,41 @@ int lde_forward(uint64_t* lde, size_t col_stride, size_t coset_stride, uint32_t 
 }
 }  // namespace
 
+namespace {
+// s' = 7 * w_{nD}^{bitrev_{log G}(P)}: the shift of shard P's sub-coset (G > D)
+uint64_t shard_shift(uint32_t log_n, uint32_t log_lde, uint32_t log_shards, uint32_t shard) {
+    const uint64_t g = gl::domain_generator(log_n + log_lde);
+    return gl::canon(gl::mul(gl::pow(g, gl::bitrev32(shard, log_shards)), gl::GENERATOR));
+}
+
+int check_shards(uint32_t log_n, uint32_t log_lde, uint32_t log_shards) {
+    if (int r = check_log_n(log_n + log_lde)) return r;
+    if (log_lde == 0) return fail(BJ_EINVAL, "lde degree must be > 1 (utils.rs:283)");
+    if (log_shards > log_n + log_lde) return fail(BJ_EINVAL, "more shards than leaves");
+    return BJ_OK;
+}
+
+// the m-point coset-s' transform of folded (bit-reversed) columns into shard P's leaf range
+int shard_from_folded(const uint64_t* folded, size_t folded_stride, uint32_t n_cols, uint32_t log_m, uint64_t sp,
+                      uint64_t* lde, hipStream_t st) {
+    const size_t m = (size_t)1 << log_m;
+    if (bj::ct_ntt_supported(log_m)) {
+        const uint64_t* tab;
+        if (int r = get_ct(log_m, false, sp, &tab)) return r;
+        HIP_TRY(bj::launch_ct(lde, m, 0, 1, folded, folded_stride, true, n_cols, log_m, tab, 0, 0, true, st),
+                "coset fft");
+        return BJ_OK;
+    }
+    const uint64_t *pyr, *lo, *hi;
+    if (int r = get_pyramid(log_m, false, &pyr)) return r;
+    if (int r = get_powers(log_m, sp, 1, &lo, &hi)) return r;
+    HIP_TRY(bj::launch_lde_forward(lde, m, 1, folded, folded_stride, true, n_cols, log_m, pyr, lo,
+                                   4096 + bj::pw_hi_len(log_m), st),
+            "coset fft");
+    return BJ_OK;
+}
+}  // namespace
+
 extern "C" {
 
 const char* bj_last_error(void) { return g_err.c_str(); }
@@ -408,9 +443,7 @@ int bj_lde_coeffs_d(const uint64_t* trace, uint32_t n_cols, size_t trace_stride,
 
 int bj_lde_shard_d(const uint64_t* coeffs, uint32_t n_cols, size_t coeffs_stride, uint32_t log_n, uint32_t log_lde,
                    uint32_t log_shards, uint32_t shard, uint64_t* work, uint64_t* lde, void* stream) {
-    if (int r = check_log_n(log_n + log_lde)) return r;
-    if (log_lde == 0) return fail(BJ_EINVAL, "lde degree must be > 1 (utils.rs:283)");
-    if (log_shards > log_n + log_lde) return fail(BJ_EINVAL, "more shards than leaves");
+    if (int r = check_shards(log_n, log_lde, log_shards)) return r;
     if (shard >= (1u << log_shards)) return fail(BJ_EINVAL, "shard index out of range");
     if (n_cols == 0) return BJ_OK;
     const size_t n = (size_t)1 << log_n;
@@ -425,24 +458,43 @@ int bj_lde_shard_d(const uint64_t* coeffs, uint32_t n_cols, size_t coeffs_stride
     if (!work) return fail(BJ_EINVAL, "work buffer required when shards exceed the lde degree");
     const uint32_t log_m = log_n - log_f;
     const size_t m = (size_t)1 << log_m;
-    // s' = 7 * w_{nD}^{bitrev_{log G}(P)}; h_t = sum_a c_{t+am} (s'^m)^a (shard.hip), then the
-    // m-point coset-s' transform of h
-    const uint64_t g = gl::domain_generator(log_n + log_lde);
-    const uint64_t sp = gl::canon(gl::mul(gl::pow(g, gl::bitrev32(shard, log_shards)), gl::GENERATOR));
+    // h_t = sum_a c_{t+am} (s'^m)^a (shard.hip), then the m-point coset-s' transform of h
+    const uint64_t sp = shard_shift(log_n, log_lde, log_shards, shard);
     HIP_TRY(bj::launch_fold(work, m, coeffs, coeffs_stride, n_cols, log_m, log_f, gl::pow(sp, m), S(stream)), "fold");
-    if (bj::ct_ntt_supported(log_m)) {
-        const uint64_t* tab;
-        if (int r = get_ct(log_m, false, sp, &tab)) return r;
-        HIP_TRY(bj::launch_ct(lde, m, 0, 1, work, m, true, n_cols, log_m, tab, 0, 0, true, S(stream)), "coset fft");
-        return BJ_OK;
-    }
-    const uint64_t *pyr, *lo, *hi;
-    if (int r = get_pyramid(log_m, false, &pyr)) return r;
-    if (int r = get_powers(log_m, sp, 1, &lo, &hi)) return r;
-    HIP_TRY(bj::launch_lde_forward(lde, m, 1, work, m, true, n_cols, log_m, pyr, lo, 4096 + bj::pw_hi_len(log_m),
-                                   S(stream)),
-            "coset fft");
+    return shard_from_folded(work, m, n_cols, log_m, sp, lde, S(stream));
+}
+
+int bj_lde_fold_shards_d(const uint64_t* coeffs, uint32_t n_cols, size_t coeffs_stride, uint32_t log_n,
+                         uint32_t log_lde, uint32_t log_shards, uint64_t* out, size_t out_shard_stride,
+                         void* stream) {
+    if (int r = check_shards(log_n, log_lde, log_shards)) return r;
+    if (log_shards <= log_lde) return fail(BJ_EINVAL, "folding needs more shards than the lde degree");
+    const uint32_t log_f = log_shards - log_lde;
+    if ((1u << log_f) > bj::kMaxFold) return fail(BJ_EINVAL, "G / D exceeds 64");
+    const uint32_t log_m = log_n - log_f;
+    const size_t m = (size_t)1 << log_m;
+    const uint32_t G = 1u << log_shards;
+    if (out_shard_stride < (size_t)n_cols * m) return fail(BJ_EINVAL, "out_shard_stride < n_cols * m");
+    if (n_cols == 0) return BJ_OK;
+    std::vector<uint64_t> spm(G);
+    for (uint32_t P = 0; P < G; P++) spm[P] = gl::pow(shard_shift(log_n, log_lde, log_shards, P), m);
+    HIP_TRY(bj::launch_fold_all(out, m, out_shard_stride, coeffs, coeffs_stride, n_cols, log_m, log_f, G, spm.data(),
+                                S(stream)),
+            "fold");
     return BJ_OK;
+}
+
+int bj_lde_shard_folded_d(const uint64_t* folded, uint32_t n_cols, size_t folded_stride, uint32_t log_n,
+                          uint32_t log_lde, uint32_t log_shards, uint32_t shard, uint64_t* lde, void* stream) {
+    if (int r = check_shards(log_n, log_lde, log_shards)) return r;
+    if (shard >= (1u << log_shards)) return fail(BJ_EINVAL, "shard index out of range");
+    if (log_shards <= log_lde) return fail(BJ_EINVAL, "folded input needs more shards than the lde degree");
+    const uint32_t log_f = log_shards - log_lde;
+    if ((1u << log_f) > bj::kMaxFold) return fail(BJ_EINVAL, "G / D exceeds 64");
+    if (n_cols == 0) return BJ_OK;
+    const uint32_t log_m = log_n - log_f;
+    return shard_from_folded(folded, folded_stride, n_cols, log_m, shard_shift(log_n, log_lde, log_shards, shard),
+                             lde, S(stream));
 }
 
 int bj_fri_fold_d(const uint64_t* c0, const uint64_t* c1, size_t n_src, const uint64_t* roots,

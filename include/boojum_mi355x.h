@@ -125,6 +125,21 @@ int bj_lde_shard_d(const uint64_t* coeffs, uint32_t n_cols, size_t coeffs_stride
                    uint32_t log_lde, uint32_t log_shards, uint32_t shard, uint64_t* work, uint64_t* lde,
                    void* stream);
 
+/* G > D with the fold moved to the sender (all-to-all exchange of m-length columns instead of
+ * an all-gather of n-length ones: n/m = G/D times fewer bytes on the wire).
+ * bj_lde_fold_shards_d (every rank, its own columns in the bj_lde_coeffs_d format): for every
+ *   shard P < G, out + P * out_shard_stride + c * m receives column c folded mod
+ *   Y^m - s_P^m, bit-reversed (the h of bj_lde_shard_d's fold step); out_shard_stride >=
+ *   n_cols * m.
+ * bj_lde_shard_folded_d (rank P, every column folded for P, gathered from all ranks): the
+ *   m-point coset transform of the folded columns, the same leaf range and layout as
+ *   bj_lde_shard_d.  folded read only. */
+int bj_lde_fold_shards_d(const uint64_t* coeffs, uint32_t n_cols, size_t coeffs_stride, uint32_t log_n,
+                         uint32_t log_lde, uint32_t log_shards, uint64_t* out, size_t out_shard_stride,
+                         void* stream);
+int bj_lde_shard_folded_d(const uint64_t* folded, uint32_t n_cols, size_t folded_stride, uint32_t log_n,
+                          uint32_t log_lde, uint32_t log_shards, uint32_t shard, uint64_t* lde, void* stream);
+
 /* ---------------------------------------------------------- Poseidon2 / Merkle */
 
 /* poseidon2_permutation (implementations/poseidon2/state_generic_impl.rs:221-249) on

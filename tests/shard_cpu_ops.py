@@ -3,7 +3,8 @@
 Lets the multi-process (gloo) tests exercise the sharded orchestration (column shards,
 all-gather order, leaf-range ownership, cap assembly incl. cap < G) on CPU tensors.
 Each step restates the same contract as the C-ABI entry point it stands in for
-(include/boojum_mi355x.h: bj_lde_coeffs_d, bj_lde_shard_d, bj_merkle_*_d)."""
+(include/boojum_mi355x.h: bj_lde_coeffs_d, bj_lde_shard_d, bj_lde_fold_shards_d,
+bj_lde_shard_folded_d, bj_merkle_*_d)."""
 import numpy as np
 
 import oracle as O
@@ -24,6 +25,35 @@ class CpuShardOps:
         # monomials in bit-reversed order
         for c in range(trace.shape[0]):
             _np(out)[c] = O.bitreverse(O.ifft_natural_to_natural(_np(trace)[c]))
+
+    @staticmethod
+    def _shard_shift(log_n, log_lde, log_shards, shard):
+        # s' = 7 * w_{nD}^{bitrev_{log G}(P)}
+        br = int(O.bitreverse(np.arange(1 << log_shards, dtype=np.uint64))[shard])
+        return O.gl_mul(O.gl_pow(O.domain_generator(log_n + log_lde), br), 7)
+
+    def fold_shards(self, coeffs, log_n, log_lde, log_shards, out):
+        # h_t = sum_a c_{t+am} (s_P^m)^a for every shard P; stored bit-reversed like the input
+        n = 1 << log_n
+        m = (n << log_lde) >> log_shards
+        f = n // m
+        for P in range(1 << log_shards):
+            z = O.gl_pow(self._shard_shift(log_n, log_lde, log_shards, P), m)
+            for c in range(coeffs.shape[0]):
+                mono = [int(x) for x in O.bitreverse(_np(coeffs)[c])]
+                h = []
+                for t in range(m):
+                    acc, zp = mono[t], 1
+                    for a in range(1, f):
+                        zp = O.gl_mul(zp, z)
+                        acc = O.gl_add(acc, O.gl_mul(mono[t + a * m], zp))
+                    h.append(acc)
+                _np(out)[P, c] = O.bitreverse(np.array(h, dtype=np.uint64))
+
+    def lde_shard_folded(self, folded, log_n, log_lde, log_shards, shard, lde):
+        sp = self._shard_shift(log_n, log_lde, log_shards, shard)
+        for c in range(folded.shape[0]):
+            _np(lde)[c] = O.fft_natural_to_bitreversed(O.bitreverse(_np(folded)[c]), int(sp))
 
     def lde_shard(self, coeffs, log_n, log_lde, log_shards, shard, work, lde):
         n = 1 << log_n

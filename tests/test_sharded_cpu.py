@@ -1,7 +1,9 @@
 """Multi-process (gloo, CPU) tests of the coset-sharded commit orchestration
 (boojum_amd/sharded.py) with the oracle standing in for the HIP steps: column-shard
 ownership (contiguous, and 8-column blocks for the column pipeline), the coefficient
-all-gather order, leaf-range ownership for G <= D (whole cosets) and G > D (sub-cosets),
+all-gather order, leaf-range ownership for G <= D (whole cosets) and G > D (sub-cosets, the
+fold either on the sender with an all-to-all -- the default -- or on the receiver after an
+all-gather),
 the sponge carried across column chunks, subtree nodes as slices of the reference tree, and
 cap assembly for cap >= G and cap < G (top levels hashed redundantly)."""
 import pytest
@@ -18,6 +20,9 @@ from sharded_check import run_and_check
     (4, (64, 4, 1, 2, 1)),    # column pipeline: 2 chunks, G > D (sub-cosets), cap < G
     (2, (48, 4, 2, 8, 1)),    # column pipeline: 3 chunks, G < D
     (2, (128, 4, 1, 4)),      # column pipeline: chunks of 1, 1, 2, 4 blocks per rank
+    (4, (4, 4, 1, 2, 0, False)),      # G > D through the all-gather of unfolded coefficients
+    (4, (64, 4, 1, 2, 1, False)),     # the same, column-pipelined
+    (8, (8, 4, 1, 16)),               # G = 4 D: fold by 4 on the sender, all-to-all
 ])
 def test_sharded_commit_gloo(world, cfg, tmp_path):
     run_and_check(world, cfg, tmp_path, "cpu")

@@ -28,18 +28,26 @@ def main():
         """sharded_witness_commit without its collectives (rank 0's compute only)."""
         ops = ws.ops
         for k, (lo, g, c) in enumerate(ws.column_runs()):
-            ops.coeffs(tr[lo:lo + c], ws.coeffs[g:g + c], ws.log_n)
+            if ws.fold_exchange:
+                ops.coeffs(tr[lo:lo + c], ws.own[lo:lo + c], ws.log_n)
+                ops.fold_shards(ws.own[lo:lo + c], ws.log_n, ws.log_lde, ws.log_g, ws.send_chunk(lo, c))
+            else:
+                ops.coeffs(tr[lo:lo + c], ws.coeffs[g:g + c], ws.log_n)
         for k in range(ws.n_chunks):
             c0, c1 = ws.chunk_columns(k)
-            work = None if ws.work is None else ws.work[:c1 - c0]
-            ops.lde_shard(ws.coeffs[c0:c1], ws.log_n, ws.log_lde, ws.log_g, ws.rank, work, ws.lde[c0:c1])
+            if ws.fold_exchange:
+                ops.lde_shard_folded(ws.folded[c0:c1], ws.log_n, ws.log_lde, ws.log_g, ws.rank, ws.lde[c0:c1])
+            else:
+                work = None if ws.work is None else ws.work[:c1 - c0]
+                ops.lde_shard(ws.coeffs[c0:c1], ws.log_n, ws.log_lde, ws.log_g, ws.rank, work, ws.lde[c0:c1])
             last = k == ws.n_chunks - 1
             ops.leaves(ws.lde[c0:c1], ws.leaves if last else ws.state, cap_in=None if k == 0 else ws.state,
                        final=last)
         ops.nodes(ws.leaves, ws.cap_local, ws.nodes)
 
-    for world in (1, 2, 4, 8):
-        ws = sharded.ShardedWorkspace(n_cols, log_n, log_lde, cap, 0, world, device="cuda")
+    runs = [(w, True) for w in (1, 2, 4, 8)] + [(w, False) for w in (8,) if w > (1 << log_lde)]
+    for world, fold in runs:
+        ws = sharded.ShardedWorkspace(n_cols, log_n, log_lde, cap, 0, world, device="cuda", fold_exchange=fold)
         tr = ws.synthetic_trace_shard()
         compute(ws, tr)   # warm-up
         torch.cuda.synchronize()
@@ -50,7 +58,7 @@ def main():
         e.record()
         torch.cuda.synchronize()
         ms = s.elapsed_time(e) / 3
-        out[world] = {"ms_per_rank": round(ms, 2), "chunks": ws.n_chunks,
+        out["%d%s" % (world, "" if fold or world <= (1 << log_lde) else "_allgather")] = {"ms_per_rank": round(ms, 2), "chunks": ws.n_chunks,
                       "ideal_elems_per_s": n_cols * (1 << log_n) / (ms * 1e-3)}
         del ws, tr
         torch.cuda.empty_cache()
