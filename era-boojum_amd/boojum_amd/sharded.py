@@ -21,42 +21,50 @@ pool). This is its multi-GPU split (BASELINE north_star):
   * the cap is all-gathered: cap/G digests per rank when cap >= G. Otherwise every rank
     all-gathers the G subtree roots and hashes the top log2(G/cap) levels redundantly.
 
-Column pipeline (C a multiple of 8 G). The leaf sponge absorbs columns in order, 8 per
-permutation, and between 8-column groups its only carried state is the 4 capacity words
-(bj_merkle_leaves_partial_d). So the columns are dealt to ranks in 8-column blocks, and the
-exchange runs as one all-gather per chunk of b_k blocks per rank (8 b_k G consecutive
-columns; b = 1, 1, 2, 4, 4, ...). Each chunk's all-gather is issued on RCCL's stream as soon
-as this rank's part of it is inverse-transformed. Chunk k's coset transform and sponge
-absorption then run on the compute stream as soon as chunk k has arrived, while later chunks
-are still on the wire. Block ownership: global 8-column block B_k*G + P*b_k + j (chunk k,
-j < b_k, B_k = b_0 + ... + b_{k-1}) belongs to rank P, at local block B_k + j. Otherwise
-(C not a multiple of 8 G) rank P holds the contiguous columns [P*C/G, (P+1)*C/G) and one
-all-gather runs before the transforms.
+Column pipeline. The leaf sponge absorbs columns in order, 8 per permutation, and between
+8-column groups its only carried state is the 4 capacity words (bj_merkle_leaves_partial_d).
+So the columns are dealt out chunk by chunk: chunk k is G c_k consecutive columns (a multiple
+of 8), of which rank P holds the P-th run of c_k; c = u, u, 2u, 4u, ... capped at
+MAX_CHUNK_COLS, u = 8 / gcd(8, G) (so the first chunk is only 8 columns wide). Each chunk's
+exchange is issued on RCCL's stream as soon as this rank's part of it is inverse-transformed
+(and folded). Chunk k's coset transform and sponge absorption then run on the compute stream
+as soon as chunk k has arrived, while later chunks are still on the wire. Rank P's run of
+chunk k is global columns [G S_k + P c_k, G S_k + (P+1) c_k), local [S_k, S_k + c_k),
+S_k = c_0 + ... + c_{k-1}. If C/G is not a multiple of u, rank P holds the contiguous
+columns [P*C/G, (P+1)*C/G) and one exchange runs before the transforms.
 
 Outputs stay sharded: each rank keeps its LDE slice, its leaves and subtree nodes, and
 the full cap. The compute steps are an `ops` object: `HipShardOps` (the C ABI on the
 GPU) is the product path and the default; the CPU multi-process tests inject a CPU
 implementation to check the orchestration with `gloo`.
 """
+import math
+
 import torch
 
 from ._lib import call
 from .field import stream_of
 
-MAX_CHUNK_BLOCKS = 4   # largest pipelined chunk, in 8-column blocks per rank
+MAX_CHUNK_COLS = 32   # largest pipelined chunk, in columns per rank
 
 
-def _chunk_schedule(blocks_per_rank, max_blocks=MAX_CHUNK_BLOCKS):
-    """Blocks per rank in each pipelined chunk: 1, 1, 2, 4, ... capped at max_blocks.  The first
-    chunks are small so little of the exchange is exposed before the pipeline fills; later
-    ones are larger so the per-chunk launch and tail costs stay small."""
-    sched, done, b = [], 0, 1
-    while done < blocks_per_rank:
-        take = min(b, blocks_per_rank - done)
+def _chunk_unit(world):
+    """Fewest columns per rank that make a chunk a whole number of 8-column sponge groups."""
+    return 8 // math.gcd(8, world)
+
+
+def _chunk_schedule(cols_per_rank, unit, max_cols=MAX_CHUNK_COLS):
+    """Columns per rank in each pipelined chunk: u, u, 2u, 4u, ... capped at max_cols (rounded
+    to a multiple of u).  The first chunks are small so little of the exchange is exposed before
+    the pipeline fills; later ones are larger so the per-chunk launch and tail costs stay small."""
+    max_cols = max(unit, max_cols // unit * unit)
+    sched, done, b = [], 0, unit
+    while done < cols_per_rank:
+        take = min(b, cols_per_rank - done)
         sched.append(take)
         done += take
         if len(sched) >= 2:
-            b = min(2 * b, max_blocks)
+            b = min(2 * b, max_cols)
     return sched
 
 
@@ -158,7 +166,7 @@ class ShardedWorkspace:
     """
 
     def __init__(self, n_cols, log_n, log_lde, cap_size, rank, world, device="cuda", group=None, ops=None,
-                 max_chunk_blocks=MAX_CHUNK_BLOCKS, fold_exchange=True):
+                 max_chunk_cols=MAX_CHUNK_COLS, fold_exchange=True):
         log_g = _log2(world)
         _log2(cap_size)
         if n_cols % world:
@@ -179,13 +187,14 @@ class ShardedWorkspace:
         if m <= self.cap_local:
             raise ValueError("each shard needs more leaves than its cap slice")
         # column pipeline geometry
-        self.pipelined = n_cols % (8 * world) == 0
+        unit = _chunk_unit(world)
+        self.pipelined = self.cols_per_rank % unit == 0
         if self.pipelined:
-            self.schedule = _chunk_schedule(n_cols // (8 * world), max_chunk_blocks)
+            self.schedule = _chunk_schedule(self.cols_per_rank, unit, max_chunk_cols)
         else:
-            self.schedule = [None]
+            self.schedule = [self.cols_per_rank]
         self.n_chunks = len(self.schedule)
-        self.chunk_cols = n_cols if not self.pipelined else 8 * world * max(self.schedule)
+        self.chunk_cols = world * max(self.schedule)
         kw = dict(dtype=torch.int64, device=device)
         self.fold_exchange = bool(fold_exchange) and log_g > log_lde
         if self.fold_exchange:
@@ -212,23 +221,23 @@ class ShardedWorkspace:
 
     def column_runs(self):
         """This rank's columns as (local_first, global_first, count) runs, one per chunk, in
-        local order.  Chunk k (b_k blocks per rank) covers global columns
-        [8 G B_k, 8 G (B_k + b_k)), B_k = sum of the earlier b; rank P owns its P-th 8 b_k slice."""
+        local order.  Chunk k (c_k columns per rank) covers global columns
+        [G S_k, G (S_k + c_k)), S_k = sum of the earlier c; rank P owns its P-th c_k slice."""
         P = self.rank
         if not self.pipelined:
             return [(0, P * self.cols_per_rank, self.cols_per_rank)]
-        runs, B = [], 0
-        for b in self.schedule:
-            runs.append((8 * B, 8 * (B * self.world + P * b), 8 * b))
-            B += b
+        runs, S = [], 0
+        for c in self.schedule:
+            runs.append((S, S * self.world + P * c, c))
+            S += c
         return runs
 
     def chunk_columns(self, k):
         """Global column range [lo, hi) of chunk k."""
         if not self.pipelined:
             return 0, self.n_cols
-        B = sum(self.schedule[:k])
-        return 8 * self.world * B, 8 * self.world * (B + self.schedule[k])
+        S = sum(self.schedule[:k])
+        return self.world * S, self.world * (S + self.schedule[k])
 
     def send_chunk(self, lo, c):
         """(G, c, m) view of the send buffer for the run of c local columns starting at lo."""

@@ -19,7 +19,7 @@ def run(rank, world, port, cfg, outdir, device, paths):
     try:
         from boojum_amd.sharded import ShardedWorkspace, sharded_witness_commit
         n_cols, log_n, log_lde, cap = cfg[:4]
-        extra = {"max_chunk_blocks": cfg[4]} if len(cfg) > 4 and cfg[4] else {}
+        extra = {"max_chunk_cols": 8 * cfg[4]} if len(cfg) > 4 and cfg[4] else {}
         if len(cfg) > 5:
             extra["fold_exchange"] = cfg[5]
         if device == "cpu":

@@ -1,6 +1,6 @@
 """Multi-process (gloo, CPU) tests of the coset-sharded commit orchestration
 (boojum_amd/sharded.py) with the oracle standing in for the HIP steps: column-shard
-ownership (contiguous, and 8-column blocks for the column pipeline), the coefficient
+ownership (contiguous, and per-chunk column runs for the column pipeline), the coefficient
 all-gather order, leaf-range ownership for G <= D (whole cosets) and G > D (sub-cosets, the
 fold either on the sender with an all-to-all -- the default -- or on the receiver after an
 all-gather),
@@ -16,10 +16,11 @@ from sharded_check import run_and_check
     (2, (2, 4, 2, 2)),    # G < D
     (4, (4, 4, 1, 2)),    # G > D (sub-cosets), cap < G
     (4, (8, 5, 2, 16)),   # G == D, cap > G
-    (2, (32, 5, 1, 4, 1)),    # column pipeline: 2 chunks of 16 columns, G == D
-    (4, (64, 4, 1, 2, 1)),    # column pipeline: 2 chunks, G > D (sub-cosets), cap < G
-    (2, (48, 4, 2, 8, 1)),    # column pipeline: 3 chunks, G < D
-    (2, (128, 4, 1, 4)),      # column pipeline: chunks of 1, 1, 2, 4 blocks per rank
+    (2, (32, 5, 1, 4, 1)),    # column pipeline: 4, 4, 8 columns per rank, G == D
+    (4, (64, 4, 1, 2, 1)),    # column pipeline: 2, 2, 4, 8 columns per rank, G > D (sub-cosets), cap < G
+    (2, (48, 4, 2, 8, 1)),    # column pipeline: 4, 4, 8, 8 columns per rank, G < D
+    (2, (128, 4, 1, 4)),      # column pipeline: 4, 4, 8, 16, 32 columns per rank
+    (8, (32, 4, 1, 16)),      # column pipeline: 1, 1, 2 columns per rank (first chunk 8 columns)
     (4, (4, 4, 1, 2, 0, False)),      # G > D through the all-gather of unfolded coefficients
     (4, (64, 4, 1, 2, 1, False)),     # the same, column-pipelined
     (8, (8, 4, 1, 16)),               # G = 4 D: fold by 4 on the sender, all-to-all
