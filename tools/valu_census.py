@@ -30,10 +30,10 @@ FULL_RATE = re.compile(r"^v_(add_u32|sub_u32|mov_b32|and_b32|or_b32|xor_b32|lshl
                        r"alignbit_b32|bfe_u32|and_or_b32|or3_b32|xad_u32|not_b32|cndmask_b32_e32)")
 
 
-def disassemble():
-    src = os.path.join(ROOT, "era-boojum_amd", "csrc", "merkle.hip")
-    dev = "/tmp/_census_merkle_dev.o"
-    co = "/tmp/_census_merkle.co"
+def disassemble(name="merkle"):
+    src = os.path.join(ROOT, "era-boojum_amd", "csrc", name + ".hip")
+    dev = "/tmp/_census_%s_dev.o" % name
+    co = "/tmp/_census_%s.co" % name
     subprocess.run([HIPCC, "-O3", "-std=c++17", "--offload-arch=gfx950", "--cuda-device-only", "-c", "-o", dev,
                     src], check=True)
     subprocess.run([os.path.join(LLVM, "clang-offload-bundler"), "--unbundle", "--type=o", "--input=" + dev,
@@ -92,6 +92,37 @@ def census(instrs, trips=(4, 11, 4)):
     return valu, slots, hist
 
 
+def straight_line(instrs):
+    """(VALU instructions, issue slots) of a kernel without loops, every instruction once."""
+    valu = slots = 0
+    for _, mn, _ in instrs:
+        if mn.startswith("v_"):
+            valu += 1
+            slots += 1 if FULL_RATE.match(mn) else 2
+    return valu, slots
+
+
+def ntt_census():
+    """Per-wave VALU instructions and issue slots of the coset-folded CT passes (ntt_ct.hip):
+    ct_head_kernel<R, MODE, KAPPA> for R = log n - 13 (forward: MODE 1, no kappa; inverse:
+    MODE 0 with kappa) and ct_tail_kernel. They are fully unrolled (no loops), so one wave
+    executes each instruction once; bench.py multiplies by the launched waves for the NTT
+    phase's VALU utilisation. (The tail's uniform canon_out branch is counted taken.)"""
+    dis = disassemble("ntt_ct")
+    out = {}
+    for r in range(5, 11):
+        for key, tmpl in (("head_fwd", "ct_head_kernelILi%dELi1ELb0E" % r), ("head_inv", "ct_head_kernelILi%dELi0ELb1E" % r)):
+            ins = parse(kernel_lines(dis, tmpl))
+            if ins:
+                v, s = straight_line(ins)
+                out.setdefault(key, {})[str(r)] = {"valu": v, "slots": s}
+    v, s = straight_line(parse(kernel_lines(dis, "ct_tail_kernel")))
+    out["tail"] = {"valu": v, "slots": s}
+    out["waves_per_block"] = 4
+    out["elements_per_block"] = 8192
+    return out
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--json")
@@ -101,7 +132,8 @@ def main():
     valu, slots, hist = census(instrs)
     res = {"kernel": "node_level_kernel (one Poseidon2 permutation per lane + 64 B in / 32 B out)",
            "valu_instr_per_perm": valu, "issue_slots_per_perm": slots,
-           "top": dict(sorted(hist.items(), key=lambda kv: -kv[1])[:12])}
+           "top": dict(sorted(hist.items(), key=lambda kv: -kv[1])[:12]),
+           "ntt_ct": ntt_census()}
     print(json.dumps(res, indent=1))
     if args.json:
         with open(args.json, "w") as f:
