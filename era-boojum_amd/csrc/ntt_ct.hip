@@ -103,6 +103,12 @@ __device__ __forceinline__ uint32_t swz_head(uint32_t e) {
     return e ^ (((e >> (5 + LOGW)) & m) << LOGW);
 }
 
+// LDS slot of the MODE 1 gather staging: XOR the low 4 bits of the 13-bit tile index with its
+// top 4 bits (the top bits of the row). A 16-lane ds_write_b64 group writes one column of 16
+// rows whose top bits are bitrev(sg) (all different), so its 16 slots are distinct mod 16;
+// a 32-lane ds_read_b64 half reads an aligned run of 32 indices, which the XOR maps onto itself.
+__device__ __forceinline__ uint32_t swz_gather(uint32_t e) { return e ^ ((e >> 9) & 15); }
+
 // Phase A' twiddles of stage v (register distance 16 >> v): pair q's group is lo(q) >> (5 - v),
 // the same for every thread.
 template <int V>
@@ -173,10 +179,10 @@ __global__ __launch_bounds__(NT, 2) void ct_head_kernel(uint64_t* dst, size_t ds
 #pragma unroll
         for (int k = 0; k < PT; k++) x[k] = sc[run + sg + T * k];
 #pragma unroll
-        for (int k = 0; k < PT; k++) lds[swz_head<LOGW>(gl::bitrev32(sg + T * k, R) * W + wg)] = x[k];
+        for (int k = 0; k < PT; k++) lds[swz_gather(gl::bitrev32(sg + T * k, R) * W + wg)] = x[k];
         __syncthreads();
 #pragma unroll
-        for (int k = 0; k < PT; k++) x[k] = lds[swz_head<LOGW>((s + T * k) * W + w)];
+        for (int k = 0; k < PT; k++) x[k] = lds[swz_gather((s + T * k) * W + w)];
     }
     // phase A': rows s + T k, stages 0..4
     {
