@@ -41,20 +41,31 @@ class CommitWorkspace:
 
     def tree(self):
         from .merkle import MerkleTreeWithCap
-        return MerkleTreeWithCap(self.cap_size, self.leaves, self.nodes)
+        return MerkleTreeWithCap(self.cap_size, self.leaves, self.nodes, getattr(self, "hasher", "poseidon2"))
 
 
-def witness_commit(trace, lde_degree, cap_size, workspace=None):
+def witness_commit(trace, lde_degree, cap_size, workspace=None, hasher="poseidon2"):
     """Commit a (C, n) int64 CUDA trace tensor.  Returns the workspace holding
     lde (C, D, n), leaves, nodes and cap (all on device, canonical).
-    Asynchronous on the current stream."""
+    Asynchronous on the current stream.  hasher: "poseidon2" (GoldilocksPoseidon2Sponge, the
+    recursive-mode tree) or "blake2s" (Blake2s256, the non-recursive one)."""
     v, c, n, stride = col_view(trace)
     log_n, log_d = _log2(n), _log2(lde_degree)
     ws = workspace or CommitWorkspace(c, log_n, log_d, cap_size, device=v.device)
     if (ws.n_cols, ws.log_n, ws.log_lde, ws.cap_size) != (c, log_n, log_d, cap_size):
         raise ValueError("workspace shape does not match the trace")
-    call("bj_lde_commit_d", v.data_ptr(), c, stride, log_n, log_d, cap_size, ws.scratch.data_ptr(),
-         ws.lde.data_ptr(), ws.leaves.data_ptr(), ws.nodes.data_ptr(), None, stream_of(v))
+    st = stream_of(v)
+    if hasher == "poseidon2":
+        call("bj_lde_commit_d", v.data_ptr(), c, stride, log_n, log_d, cap_size, ws.scratch.data_ptr(),
+             ws.lde.data_ptr(), ws.leaves.data_ptr(), ws.nodes.data_ptr(), None, st)
+    elif hasher == "blake2s":
+        nl = n << log_d
+        call("bj_lde_d", v.data_ptr(), c, stride, log_n, log_d, ws.scratch.data_ptr(), ws.lde.data_ptr(), st)
+        call("bj_blake2s_leaves_d", ws.lde.data_ptr(), c, nl, nl, ws.leaves.data_ptr(), st)
+        call("bj_blake2s_nodes_d", ws.leaves.data_ptr(), nl, cap_size, ws.nodes.data_ptr(), st)
+    else:
+        raise ValueError("unknown tree hasher %r" % (hasher,))
+    ws.hasher = hasher
     return ws
 
 
@@ -84,7 +95,7 @@ class OracleCommitment:
         return self.tree.get_cap()
 
 
-def commit_trace_columns(trace, lde_degree, fri_lde_factor, cap_size):
+def commit_trace_columns(trace, lde_degree, fri_lde_factor, cap_size, hasher="poseidon2"):
     """Base-field columns (C, n) in Lagrange (trace) form: iFFT, coset LDE at lde_degree, tree
     over the first fri_lde_factor cosets.  The witness oracle (prover.rs:316-347) and the setup
     oracle (setup.rs:1146-1204, setup_storage.rs:18-70) are this call."""
@@ -93,11 +104,13 @@ def commit_trace_columns(trace, lde_degree, fri_lde_factor, cap_size):
     if fri_lde_factor > lde_degree:
         raise ValueError("fri_lde_factor exceeds the LDE degree")
     lde = transform_raw_storages_to_lde(trace, lde_degree)
-    return OracleCommitment(lde, MerkleTreeWithCap.construct(lde, cap_size, num_cosets=fri_lde_factor))
+    return OracleCommitment(lde, MerkleTreeWithCap.construct(lde, cap_size, num_cosets=fri_lde_factor,
+                                                             hasher=hasher))
 
 
 def second_stage_commit(z_poly, intermediate_polys, lookup_witness_encoding_polys,
-                        lookup_multiplicities_encoding_polys, lde_degree, fri_lde_factor, cap_size):
+                        lookup_multiplicities_encoding_polys, lde_degree, fri_lde_factor, cap_size,
+                        hasher="poseidon2"):
     """SecondStageProductsStorage::from_base_trace_ext + the stage-2 tree (prover.rs:505-554).
     Every argument is a GoldilocksExt2 polynomial as a (c0, c1) pair of (n,) base columns in
     Lagrange form (or a list of such pairs); the leaf order is z, intermediates, lookup witness
@@ -107,13 +120,13 @@ def second_stage_commit(z_poly, intermediate_polys, lookup_witness_encoding_poly
         for c0, c1 in group:
             cols += [c0, c1]
     trace = torch.stack([torch.as_tensor(c) for c in cols])
-    return commit_trace_columns(trace, lde_degree, fri_lde_factor, cap_size)
+    return commit_trace_columns(trace, lde_degree, fri_lde_factor, cap_size, hasher=hasher)
 
 
-def quotient_commit(monomials, fri_lde_factor, cap_size):
+def quotient_commit(monomials, fri_lde_factor, cap_size, hasher="poseidon2"):
     """Quotient chunks already in monomial form (prover.rs:1454-1495): transform_monomials_to_lde
     at fri_lde_factor, then the tree over all its cosets."""
     from .lde import transform_monomials_to_lde
     from .merkle import MerkleTreeWithCap
     lde = transform_monomials_to_lde(monomials, fri_lde_factor)
-    return OracleCommitment(lde, MerkleTreeWithCap.construct(lde, cap_size))
+    return OracleCommitment(lde, MerkleTreeWithCap.construct(lde, cap_size, hasher=hasher))

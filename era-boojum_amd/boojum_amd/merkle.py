@@ -1,9 +1,11 @@
-"""MerkleTreeWithCap / TreeHasher over the Poseidon2 Overwrite sponge.
+"""MerkleTreeWithCap / TreeHasher over the Poseidon2 Overwrite sponge or Blake2s256.
 
 Mirrors cs/oracle/merkle_tree.rs (construct :78-172, continue_from_leaf_hashes
 :388-449, get_cap :451-460, get_proof :462-480, verify_proof_over_cap :482-504) and the
-TreeHasher impl for GoldilocksPoseidon2Sponge<AbsorptionModeOverwrite>
-(cs/oracle/mod.rs:114-175).  Digests are [u64; 4], canonical.
+TreeHasher impls for GoldilocksPoseidon2Sponge<AbsorptionModeOverwrite>
+(cs/oracle/mod.rs:114-175; digests [u64; 4], canonical) and blake2::Blake2s256
+(:177-246; digests [u8; 32], held as 4 little-endian u64 words).  `hasher` selects one:
+"poseidon2" (the default, the recursive-mode tree) or "blake2s".
 
 Device layout: leaf_hashes (n_leaves, 4); node levels concatenated from the leaves up
 to the cap, (n_leaves - cap_size, 4) -- the reference's node_hashes_enumerated_from_leafs
@@ -50,6 +52,41 @@ class Poseidon2Sponge:
         return s
 
 
+class Blake2s256:
+    """TreeHasher<GoldilocksField> for blake2::Blake2s256 (host-call forms). Digests are 32
+    bytes as 4 little-endian u64 words (`digest_bytes` gives the bytes)."""
+
+    @staticmethod
+    def hash_into_leaf(elements):
+        e = as_u64_host(elements)
+        out = np.zeros(4, dtype=np.uint64)
+        call("bj_blake2s_leaf_h", _hp(e) if e.size else None, e.size, _hp(out))
+        return out
+
+    @staticmethod
+    def hash_into_node(left, right, depth=0):
+        out = np.zeros(4, dtype=np.uint64)
+        call("bj_blake2s_node_h", _hp(as_u64_host(left)), _hp(as_u64_host(right)), _hp(out))
+        return out
+
+    @staticmethod
+    def digest_bytes(words):
+        return np.asarray(words, dtype=np.uint64).astype("<u8").tobytes()
+
+
+# hasher name -> (host TreeHasher, leaves, chunked leaves, nodes entry points)
+HASHERS = {
+    "poseidon2": (Poseidon2Sponge, "bj_merkle_leaves_d", "bj_merkle_leaves_chunked_d", "bj_merkle_nodes_d"),
+    "blake2s": (Blake2s256, "bj_blake2s_leaves_d", "bj_blake2s_leaves_chunked_d", "bj_blake2s_nodes_d"),
+}
+
+
+def _hasher(name):
+    if name not in HASHERS:
+        raise ValueError("unknown tree hasher %r (expected one of %s)" % (name, sorted(HASHERS)))
+    return HASHERS[name]
+
+
 def _log2(n):
     if n <= 0 or n & (n - 1):
         raise ValueError("size must be a power of two, got %d" % n)
@@ -78,13 +115,16 @@ def _leaf_sources(leafs_sources, num_cosets=None):
 
 
 class MerkleTreeWithCap:
-    def __init__(self, cap_size, leaf_hashes, nodes):
+    def __init__(self, cap_size, leaf_hashes, nodes, hasher="poseidon2"):
+        _hasher(hasher)
         self.cap_size = cap_size
         self.leaf_hashes = leaf_hashes            # (n_leaves, 4) int64 CUDA tensor
         self.nodes = nodes                        # (n_leaves - cap_size, 4)
+        self.hasher = hasher
 
     @classmethod
-    def construct(cls, leafs_sources, cap_size, num_cosets=None, leaf_out=None, node_out=None):
+    def construct(cls, leafs_sources, cap_size, num_cosets=None, leaf_out=None, node_out=None, hasher="poseidon2"):
+        _, f_leaves, _, f_nodes = _hasher(hasher)
         src, c, stride, nl = _leaf_sources(leafs_sources, num_cosets)
         _log2(nl)
         _log2(cap_size)
@@ -94,12 +134,12 @@ class MerkleTreeWithCap:
         leaves = leaf_out if leaf_out is not None else torch.empty((nl, 4), dtype=torch.int64, device=dev)
         nodes = node_out if node_out is not None else torch.empty((nl - cap_size, 4), dtype=torch.int64, device=dev)
         st = stream_of(src)
-        call("bj_merkle_leaves_d", src.data_ptr(), c, stride, nl, leaves.data_ptr(), st)
-        call("bj_merkle_nodes_d", leaves.data_ptr(), nl, cap_size, nodes.data_ptr(), st)
-        return cls(cap_size, leaves, nodes)
+        call(f_leaves, src.data_ptr(), c, stride, nl, leaves.data_ptr(), st)
+        call(f_nodes, leaves.data_ptr(), nl, cap_size, nodes.data_ptr(), st)
+        return cls(cap_size, leaves, nodes, hasher)
 
     @classmethod
-    def construct_by_chunking(cls, leafs_sources, elements_to_take_per_leaf, cap_size):
+    def construct_by_chunking(cls, leafs_sources, elements_to_take_per_leaf, cap_size, hasher="poseidon2"):
         """merkle_tree.rs:176-306 (the FRI base oracle, fri/mod.rs:179-187): leaf j of the flat
         tree hashes, for each source in order, elements [j*E, (j+1)*E) of its flat LDE (cosets
         in order). leafs_sources: (C, D, n) LDE tensor or (C, L) flat rows."""
@@ -114,10 +154,11 @@ class MerkleTreeWithCap:
             raise ValueError("each coset must hold whole leaves (merkle_tree.rs:197-198)")
         if nl <= cap_size:
             raise ValueError("tree size must exceed cap size (merkle_tree.rs:207)")
-        return cls._chunked(src, c, stride, nl, e, cap_size)
+        return cls._chunked(src, c, stride, nl, e, cap_size, hasher)
 
     @classmethod
-    def construct_by_chunking_from_flat_sources(cls, leafs_sources, elements_to_take_per_leaf, cap_size):
+    def construct_by_chunking_from_flat_sources(cls, leafs_sources, elements_to_take_per_leaf, cap_size,
+                                                hasher="poseidon2"):
         """merkle_tree.rs:308-386 (FRI intermediate oracles, fri/mod.rs:258-266): as
         construct_by_chunking over flat (C, N) sources; tree_size == cap_size is allowed (the
         cap is then the leaf layer)."""
@@ -130,19 +171,20 @@ class MerkleTreeWithCap:
         nl = total // e
         if nl < cap_size:
             raise ValueError("trying to make tree of size %d with cap %d" % (nl, cap_size))
-        return cls._chunked(src, c, stride, nl, e, cap_size)
+        return cls._chunked(src, c, stride, nl, e, cap_size, hasher)
 
     @classmethod
-    def _chunked(cls, src, c, stride, nl, e, cap_size):
+    def _chunked(cls, src, c, stride, nl, e, cap_size, hasher):
+        _, _, f_chunked, f_nodes = _hasher(hasher)
         _log2(nl)
         dev = src.device
         leaves = torch.empty((nl, 4), dtype=torch.int64, device=dev)
         nodes = torch.empty((nl - cap_size, 4), dtype=torch.int64, device=dev)
         st = stream_of(src)
-        call("bj_merkle_leaves_chunked_d", src.data_ptr(), c, stride, nl, e, leaves.data_ptr(), st)
+        call(f_chunked, src.data_ptr(), c, stride, nl, e, leaves.data_ptr(), st)
         if nl > cap_size:
-            call("bj_merkle_nodes_d", leaves.data_ptr(), nl, cap_size, nodes.data_ptr(), st)
-        return cls(cap_size, leaves, nodes)
+            call(f_nodes, leaves.data_ptr(), nl, cap_size, nodes.data_ptr(), st)
+        return cls(cap_size, leaves, nodes, hasher)
 
     @property
     def n_leaves(self):
@@ -178,14 +220,15 @@ class MerkleTreeWithCap:
         return leaf, np.array(path, dtype=np.uint64).reshape(depth, 4)
 
     @staticmethod
-    def verify_proof_over_cap(proof, cap, leaf_hash, idx):
+    def verify_proof_over_cap(proof, cap, leaf_hash, idx, hasher="poseidon2"):
         """merkle_tree.rs:482-504 (host; one node hash per level through the library)."""
+        H = _hasher(hasher)[0]
         cur = as_u64_host(leaf_hash)
         for el in np.asarray(proof, dtype=np.uint64).reshape(-1, 4):
             if idx & 1 == 0:
-                cur = Poseidon2Sponge.hash_into_node(cur, el)
+                cur = H.hash_into_node(cur, el)
             else:
-                cur = Poseidon2Sponge.hash_into_node(el, cur)
+                cur = H.hash_into_node(el, cur)
             idx >>= 1
         cap = np.asarray(cap, dtype=np.uint64).reshape(-1, 4)
         return bool(np.array_equal(cap[idx], cur))

@@ -188,6 +188,32 @@ int bj_merkle_leaves_partial_d(const uint64_t* src, uint32_t n_cols, size_t col_
 int bj_merkle_nodes_d(const uint64_t* leaves, size_t n_leaves, uint32_t cap_size, uint64_t* nodes,
                       void* stream);
 
+/* ------------------------------------------------ Blake2s256 tree hasher */
+/* MerkleTreeWithCap<GoldilocksField, blake2::Blake2s256>: the TreeHasher impl of
+ * cs/oracle/mod.rs:177-246, used by the non-recursive prover configs
+ * (gadgets/sha256/mod.rs:263-269).  Leaf = BLAKE2s-256 (RFC 7693, no key) of the canonical
+ * little-endian bytes of the leaf's elements (as_u64_reduced().to_le_bytes(), :194-197);
+ * node = BLAKE2s-256(left || right) (:233-245).  A digest is 32 bytes, stored as 4
+ * little-endian u64 words, so leaves / nodes use the same (N x 4) layout as the Poseidon2
+ * tree.  Same arguments, layouts and preconditions as the bj_merkle_* calls above. */
+int bj_blake2s_leaves_d(const uint64_t* src, uint32_t n_cols, size_t col_stride, size_t n_leaves,
+                        uint64_t* leaves, void* stream);
+int bj_blake2s_leaves_chunked_d(const uint64_t* src, uint32_t n_cols, size_t col_stride, size_t n_leaves,
+                                uint32_t elems_per_leaf, uint64_t* out, void* stream);
+int bj_blake2s_nodes_d(const uint64_t* leaves, size_t n_leaves, uint32_t cap_size, uint64_t* nodes,
+                       void* stream);
+/* Column-range continuation (the column pipeline): the carried state is the 32-byte chaining
+ * value h plus the byte count, which is 8 * cols_before (a multiple of 64).  state_in: NULL iff
+ * cols_before == 0.  final_ == 0: n_cols a multiple of 8, out = chaining values (n_leaves x 4);
+ * final_ != 0: out = digests, and n_cols > 0 when cols_before > 0 (the message's last block
+ * must be in this range). */
+int bj_blake2s_leaves_partial_d(const uint64_t* src, uint32_t n_cols, size_t col_stride, size_t n_leaves,
+                                uint64_t cols_before, const uint64_t* state_in, uint64_t* out, int final_,
+                                void* stream);
+/* host seams (TreeHasher::hash_into_leaf / hash_into_node) */
+int bj_blake2s_leaf_h(const uint64_t* elems, size_t n_elems, uint64_t* out4);
+int bj_blake2s_node_h(const uint64_t* left4, const uint64_t* right4, uint64_t* out4);
+
 /* ------------------------------------------------------- whole commitment */
 
 /* Witness commitment, the batched hot path (prover.rs:313-353 with all D cosets

@@ -366,22 +366,129 @@ void bjo_hash_into_node(const u64* l, const u64* r, u64* out4) {
     for (int i = 0; i < 4; i++) out4[i] = gl_canon(s[i]);
 }
 
+/* ------------------------------------------- Blake2s256 tree hasher (a18') */
+
+/* TreeHasher for blake2::Blake2s256 (cs/oracle/mod.rs:177-246), the tree hasher of the
+ * non-recursive prover configs (gadgets/sha256/mod.rs:263-269).  Third-party crate
+ * blake2 = "0.10" (Cargo.toml:23, resolved 0.10.6): Blake2s256 = BLAKE2s with a 32-byte
+ * digest, no key, salt or personalisation, i.e. RFC 7693 (restated below).
+ *   leaf: update(as_u64_reduced(x).to_le_bytes()) for each element, finalize (:187-231);
+ *   node: update(left 32 B), update(right 32 B), finalize (:233-245).
+ * Digests are 32 bytes, stored here as 4 little-endian u64 words. */
+static const uint32_t B2S_IV[8] = {0x6A09E667u, 0xBB67AE85u, 0x3C6EF372u, 0xA54FF53Au,
+                                   0x510E527Fu, 0x9B05688Cu, 0x1F83D9ABu, 0x5BE0CD19u};
+static const uint8_t B2S_SIGMA[10][16] = {
+    {0, 1, 2, 3, 4, 5, 6, 7, 8, 9, 10, 11, 12, 13, 14, 15}, {14, 10, 4, 8, 9, 15, 13, 6, 1, 12, 0, 2, 11, 7, 5, 3},
+    {11, 8, 12, 0, 5, 2, 15, 13, 10, 14, 3, 6, 7, 1, 9, 4}, {7, 9, 3, 1, 13, 12, 11, 14, 2, 6, 5, 10, 4, 0, 15, 8},
+    {9, 0, 5, 7, 2, 4, 10, 15, 14, 1, 11, 12, 6, 8, 3, 13}, {2, 12, 6, 10, 0, 11, 8, 3, 4, 13, 7, 5, 15, 14, 1, 9},
+    {12, 5, 1, 15, 14, 13, 4, 10, 0, 7, 6, 3, 9, 2, 8, 11}, {13, 11, 7, 14, 12, 1, 3, 9, 5, 0, 15, 4, 8, 6, 2, 10},
+    {6, 15, 14, 9, 11, 3, 0, 8, 12, 2, 13, 7, 1, 4, 10, 5}, {10, 2, 8, 4, 7, 6, 1, 5, 15, 11, 9, 14, 3, 12, 13, 0}};
+
+static inline uint32_t rotr32(uint32_t x, int r) { return (x >> r) | (x << (32 - r)); }
+
+/* RFC 7693 section 3.2, function F (10 rounds of G over the 4x4 state) */
+static void b2s_compress(uint32_t h[8], const uint32_t m[16], uint64_t t, int last) {
+    uint32_t v[16];
+    for (int i = 0; i < 8; i++) { v[i] = h[i]; v[8 + i] = B2S_IV[i]; }
+    v[12] ^= (uint32_t)t;
+    v[13] ^= (uint32_t)(t >> 32);
+    if (last) v[14] = ~v[14];
+#define B2S_G(a, b, c, d, x, y)                    \
+    do {                                           \
+        v[a] = v[a] + v[b] + x; v[d] = rotr32(v[d] ^ v[a], 16); \
+        v[c] = v[c] + v[d];     v[b] = rotr32(v[b] ^ v[c], 12); \
+        v[a] = v[a] + v[b] + y; v[d] = rotr32(v[d] ^ v[a], 8);  \
+        v[c] = v[c] + v[d];     v[b] = rotr32(v[b] ^ v[c], 7);  \
+    } while (0)
+    for (int r = 0; r < 10; r++) {
+        const uint8_t* s = B2S_SIGMA[r];
+        B2S_G(0, 4, 8, 12, m[s[0]], m[s[1]]);
+        B2S_G(1, 5, 9, 13, m[s[2]], m[s[3]]);
+        B2S_G(2, 6, 10, 14, m[s[4]], m[s[5]]);
+        B2S_G(3, 7, 11, 15, m[s[6]], m[s[7]]);
+        B2S_G(0, 5, 10, 15, m[s[8]], m[s[9]]);
+        B2S_G(1, 6, 11, 12, m[s[10]], m[s[11]]);
+        B2S_G(2, 7, 8, 13, m[s[12]], m[s[13]]);
+        B2S_G(3, 4, 9, 14, m[s[14]], m[s[15]]);
+    }
+#undef B2S_G
+    for (int i = 0; i < 8; i++) h[i] ^= v[i] ^ v[8 + i];
+}
+
+static inline uint32_t load_le32(const uint8_t* p) {
+    return (uint32_t)p[0] | ((uint32_t)p[1] << 8) | ((uint32_t)p[2] << 16) | ((uint32_t)p[3] << 24);
+}
+
+/* BLAKE2s-256 of len bytes (RFC 7693 section 3.3): every block but the last is compressed
+ * as more data follows; the last (zero-padded, possibly empty) carries the final flag and
+ * the total byte count. */
+void bjo_blake2s(const uint8_t* data, size_t len, uint8_t* out32) {
+    uint32_t h[8];
+    for (int i = 0; i < 8; i++) h[i] = B2S_IV[i];
+    h[0] ^= 0x01010000u ^ 32u; /* depth 1, fanout 1, no key, 32-byte digest */
+    uint32_t m[16];
+    size_t off = 0;
+    while (len - off > 64) {
+        for (int i = 0; i < 16; i++) m[i] = load_le32(data + off + 4 * i);
+        off += 64;
+        b2s_compress(h, m, off, 0);
+    }
+    uint8_t last[64] = {0};
+    memcpy(last, data + off, len - off);
+    for (int i = 0; i < 16; i++) m[i] = load_le32(last + 4 * i);
+    b2s_compress(h, m, len, 1);
+    for (int i = 0; i < 8; i++) {
+        out32[4 * i] = (uint8_t)h[i];
+        out32[4 * i + 1] = (uint8_t)(h[i] >> 8);
+        out32[4 * i + 2] = (uint8_t)(h[i] >> 16);
+        out32[4 * i + 3] = (uint8_t)(h[i] >> 24);
+    }
+}
+
+static void b2s_leaf_strided(const u64* elems, size_t count, size_t stride, u64* out4) {
+    uint8_t stackbuf[8 * 64] = {0};
+    uint8_t* buf = count <= 64 ? stackbuf : (uint8_t*)malloc(8 * count);
+    for (size_t i = 0; i < count; i++) {
+        u64 v = gl_canon(elems[i * stride]); /* as_u64_reduced().to_le_bytes() */
+        for (int b = 0; b < 8; b++) buf[8 * i + b] = (uint8_t)(v >> (8 * b));
+    }
+    bjo_blake2s(buf, 8 * count, (uint8_t*)out4); /* little-endian host: bytes == LE words */
+    if (buf != stackbuf) free(buf);
+}
+
+void bjo_blake2s_leaf(const u64* elems, size_t count, u64* out4) { b2s_leaf_strided(elems, count, 1, out4); }
+
+void bjo_blake2s_node(const u64* l, const u64* r, u64* out4) {
+    uint8_t buf[64];
+    memcpy(buf, l, 32);
+    memcpy(buf + 32, r, 32);
+    bjo_blake2s(buf, 64, (uint8_t*)out4);
+}
+
 /* ------------------------------------------------------------ Merkle (a19) */
 
+/* tree hashers: 0 = GoldilocksPoseidon2Sponge<AbsorptionModeOverwrite>, 1 = Blake2s256 */
 typedef struct {
     const u64* lde; size_t col_stride; uint32_t n_cols; u64* leaves;
-    const u64* prev; u64* next;
+    const u64* prev; u64* next; int hasher;
 } mk_ctx_t;
+
+static void hash_node_h(int hasher, const u64* l, const u64* r, u64* out4) {
+    if (hasher == 1) bjo_blake2s_node(l, r, out4);
+    else bjo_hash_into_node(l, r, out4);
+}
 
 static void leaf_job(void* c, size_t b, size_t e) {
     mk_ctx_t* x = (mk_ctx_t*)c;
-    for (size_t L = b; L < e; L++)
-        leaf_hash_strided(x->lde + L, x->n_cols, x->col_stride, x->leaves + 4 * L);
+    for (size_t L = b; L < e; L++) {
+        if (x->hasher == 1) b2s_leaf_strided(x->lde + L, x->n_cols, x->col_stride, x->leaves + 4 * L);
+        else leaf_hash_strided(x->lde + L, x->n_cols, x->col_stride, x->leaves + 4 * L);
+    }
 }
 
 static void node_job(void* c, size_t b, size_t e) {
     mk_ctx_t* x = (mk_ctx_t*)c;
-    for (size_t i = b; i < e; i++) bjo_hash_into_node(x->prev + 8 * i, x->prev + 8 * i + 4, x->next + 4 * i);
+    for (size_t i = b; i < e; i++) hash_node_h(x->hasher, x->prev + 8 * i, x->prev + 8 * i + 4, x->next + 4 * i);
 }
 
 /* MerkleTreeWithCap::construct, cs/oracle/merkle_tree.rs:78-172.
@@ -392,9 +499,9 @@ static void node_job(void* c, size_t b, size_t e) {
  * leaves: n_leaves x 4.  nodes: all node levels from the leaves up to and including
  * the cap level, concatenated (n_leaves/2 + n_leaves/4 + ... + cap_size) x 4
  * (node_hashes_enumerated_from_leafs, :388-449).  Returns the number of node levels. */
-int bjo_merkle_construct(const u64* lde, size_t col_stride, uint32_t n_cols, size_t n_leaves,
-                         uint32_t cap_size, u64* leaves, u64* nodes, int threads) {
-    mk_ctx_t x = {lde, col_stride, n_cols, leaves, NULL, NULL};
+int bjo_merkle_construct_with(const u64* lde, size_t col_stride, uint32_t n_cols, size_t n_leaves,
+                              uint32_t cap_size, u64* leaves, u64* nodes, int threads, int hasher) {
+    mk_ctx_t x = {lde, col_stride, n_cols, leaves, NULL, NULL, hasher};
     worker_scope(threads, n_leaves, leaf_job, &x);
     int levels = 0;
     const u64* prev = leaves;
@@ -405,6 +512,11 @@ int bjo_merkle_construct(const u64* lde, size_t col_stride, uint32_t n_cols, siz
         prev = out; out += 4 * (len / 2); levels++;
     }
     return levels;
+}
+
+int bjo_merkle_construct(const u64* lde, size_t col_stride, uint32_t n_cols, size_t n_leaves,
+                         uint32_t cap_size, u64* leaves, u64* nodes, int threads) {
+    return bjo_merkle_construct_with(lde, col_stride, n_cols, n_leaves, cap_size, leaves, nodes, threads, 0);
 }
 
 /* get_proof, merkle_tree.rs:462-480.  Writes `levels` sibling digests. */
@@ -421,18 +533,28 @@ void bjo_merkle_get_proof(const u64* leaves, const u64* nodes, size_t n_leaves, 
     }
 }
 
-/* verify_proof_over_cap, merkle_tree.rs:482-504 */
-int bjo_verify_proof_over_cap(const u64* path, int levels, const u64* cap, const u64* leaf4, size_t idx) {
+/* verify_proof_over_cap, merkle_tree.rs:482-504 (digests compared after normalize_output:
+ * canonical field elements for Poseidon2, the raw bytes for Blake2s) */
+int bjo_verify_proof_over_cap_with(const u64* path, int levels, const u64* cap, const u64* leaf4, size_t idx,
+                                   int hasher) {
     u64 cur[4], tmp[4];
     for (int i = 0; i < 4; i++) cur[i] = leaf4[i];
     for (int l = 0; l < levels; l++) {
-        if ((idx & 1) == 0) bjo_hash_into_node(cur, path + 4 * l, tmp);
-        else bjo_hash_into_node(path + 4 * l, cur, tmp);
+        if ((idx & 1) == 0) hash_node_h(hasher, cur, path + 4 * l, tmp);
+        else hash_node_h(hasher, path + 4 * l, cur, tmp);
         memcpy(cur, tmp, sizeof(cur));
         idx >>= 1;
     }
-    for (int i = 0; i < 4; i++) if (gl_canon(cap[4 * idx + i]) != gl_canon(cur[i])) return 0;
+    for (int i = 0; i < 4; i++) {
+        u64 a = cap[4 * idx + i], b = cur[i];
+        if (hasher == 0) { a = gl_canon(a); b = gl_canon(b); }
+        if (a != b) return 0;
+    }
     return 1;
+}
+
+int bjo_verify_proof_over_cap(const u64* path, int levels, const u64* cap, const u64* leaf4, size_t idx) {
+    return bjo_verify_proof_over_cap_with(path, levels, cap, leaf4, idx, 0);
 }
 
 /* ---------------------------------------------------- whole commit (a21) */

@@ -51,6 +51,13 @@ def lib():
         L.bjo_verify_proof_over_cap.argtypes = [_u64p, i, _u64p, _u64p, sz]
         L.bjo_lde_commit.restype = i
         L.bjo_lde_commit.argtypes = [_u64p, u32, u32, u32, u32, _u64p, _u64p, _u64p, _u64p, i]
+        L.bjo_blake2s.argtypes = [ctypes.c_char_p, sz, ctypes.c_char_p]
+        L.bjo_blake2s_leaf.argtypes = [_u64p, sz, _u64p]
+        L.bjo_blake2s_node.argtypes = [_u64p, _u64p, _u64p]
+        L.bjo_merkle_construct_with.restype = i
+        L.bjo_merkle_construct_with.argtypes = [_u64p, sz, u32, sz, u32, _u64p, _u64p, i, i]
+        L.bjo_verify_proof_over_cap_with.restype = i
+        L.bjo_verify_proof_over_cap_with.argtypes = [_u64p, i, _u64p, _u64p, sz, i]
         L.bjo_find_query_index.restype = ctypes.c_long
         L.bjo_find_query_index.argtypes = [_u64p, _u64p, i, _u64p, sz]
         _LIB = L
@@ -168,26 +175,59 @@ def hash_into_node(left, right):
     return out
 
 
+HASHERS = {"poseidon2": 0, "blake2s": 1}
+
+
+def blake2s(data):
+    """BLAKE2s-256 (RFC 7693) of a bytes object: the blake2 crate's Blake2s256."""
+    data = bytes(data)
+    out = ctypes.create_string_buffer(32)
+    lib().bjo_blake2s(data, len(data), out)
+    return out.raw
+
+
+def blake2s_leaf(elems):
+    """TreeHasher::hash_into_leaf for Blake2s256 (cs/oracle/mod.rs:204-216): the canonical
+    little-endian bytes of each element.  Digest as 4 little-endian u64 words."""
+    e = _u64(elems)
+    n = e.size
+    if n == 0:
+        e = np.zeros(1, np.uint64)
+    out = np.zeros(4, dtype=np.uint64)
+    lib().bjo_blake2s_leaf(_p(e), n, _p(out))
+    return out
+
+
+def blake2s_node(left, right):
+    """TreeHasher::hash_into_node for Blake2s256 (cs/oracle/mod.rs:233-245)."""
+    out = np.zeros(4, dtype=np.uint64)
+    lib().bjo_blake2s_node(_p(_u64(left)), _p(_u64(right)), _p(out))
+    return out
+
+
 def num_node_levels(n_leaves, cap_size):
     return (n_leaves.bit_length() - 1) - (cap_size.bit_length() - 1)
 
 
-def merkle_construct(lde_flat, cap_size, threads=1):
+def merkle_construct(lde_flat, cap_size, threads=1, hasher="poseidon2"):
     """lde_flat: (C, n_leaves) uint64 (column c's values over the flat leaf index).
-    Returns (leaves (n_leaves, 4), nodes (sum of levels, 4), levels, cap (cap_size, 4))."""
+    Returns (leaves (n_leaves, 4), nodes (sum of levels, 4), levels, cap (cap_size, 4)).
+    hasher: "poseidon2" (GoldilocksPoseidon2Sponge) or "blake2s" (Blake2s256, digests as
+    4 little-endian u64 words)."""
     src = _u64(lde_flat)
     c, nl = src.shape
     levels = num_node_levels(nl, cap_size)
     leaves = np.zeros((nl, 4), dtype=np.uint64)
     n_nodes = nl - cap_size if levels > 0 else 0
     nodes = np.zeros((max(n_nodes, 1), 4), dtype=np.uint64)
-    got = lib().bjo_merkle_construct(_p(src), nl, c, nl, cap_size, _p(leaves), _p(nodes), threads)
+    got = lib().bjo_merkle_construct_with(_p(src), nl, c, nl, cap_size, _p(leaves), _p(nodes), threads,
+                                          HASHERS[hasher])
     assert got == levels
     cap = nodes[n_nodes - cap_size: n_nodes].copy() if levels > 0 else leaves.copy()
     return leaves, nodes[:n_nodes], levels, cap
 
 
-def merkle_construct_by_chunking(sources_flat, elements_per_leaf, cap_size, threads=1):
+def merkle_construct_by_chunking(sources_flat, elements_per_leaf, cap_size, threads=1, hasher="poseidon2"):
     """MerkleTreeWithCap::construct_by_chunking / construct_by_chunking_from_flat_sources
     (merkle_tree.rs:176-386): leaf L hashes, for each source c in order, the E consecutive
     elements sources[c][L*E .. (L+1)*E).  Restated as an ordinary tree over C*E rows, row
@@ -197,7 +237,7 @@ def merkle_construct_by_chunking(sources_flat, elements_per_leaf, cap_size, thre
     e = elements_per_leaf
     nl = total // e
     rows = np.ascontiguousarray(src.reshape(c, nl, e).transpose(0, 2, 1).reshape(c * e, nl))
-    return merkle_construct(rows, cap_size, threads=threads)
+    return merkle_construct(rows, cap_size, threads=threads, hasher=hasher)
 
 
 def merkle_get_proof(leaves, nodes, levels, idx):
@@ -209,10 +249,11 @@ def merkle_get_proof(leaves, nodes, levels, idx):
     return leaf, path[:levels]
 
 
-def verify_proof_over_cap(path, cap, leaf, idx):
+def verify_proof_over_cap(path, cap, leaf, idx, hasher="poseidon2"):
     path = _u64(path).reshape(-1, 4)
     pp = path if path.size else np.zeros((1, 4), np.uint64)
-    return bool(lib().bjo_verify_proof_over_cap(_p(pp), path.shape[0], _p(_u64(cap)), _p(_u64(leaf)), idx))
+    return bool(lib().bjo_verify_proof_over_cap_with(_p(pp), path.shape[0], _p(_u64(cap)), _p(_u64(leaf)), idx,
+                                                     HASHERS[hasher]))
 
 
 def lde_commit(trace, log_d, cap_size, threads=1):
