@@ -134,6 +134,33 @@ def test_host_seam_in_place(bj):
     eq(bj.fft.precompute_twiddles_for_fft_host(1 << 10, True), O.precompute_twiddles(10, True))
 
 
+def test_host_seams_concurrent_threads(bj):
+    """The PrimeFieldLikeVectorized seam is driven from rayon worker threads, one column per
+    call, in place and concurrently (utils.rs:295-304, 363-379). 8 host threads call the
+    per-column seams at once (ctypes drops the GIL), on sizes 2^10..2^19 and both NTT paths,
+    with first-use table creation racing; every result must equal the oracle's."""
+    from concurrent.futures import ThreadPoolExecutor
+    jobs = []
+    for k in range(24):
+        log_n = (10, 14, 18, 19)[k % 4]
+        x = rand(1 << log_n, 1000 + k)
+        coset = (1, 7, 11, 0x1234567)[k % 4]
+        jobs.append((k, x, coset))
+
+    def run(job):
+        k, x, coset = job
+        y = x.copy()
+        if k % 2 == 0:
+            bj.fft.fft_natural_to_bitreversed_host(y, coset)
+            return y, O.fft_natural_to_bitreversed(x, coset)
+        bj.fft.ifft_natural_to_natural_host(y, coset)
+        return y, O.ifft_natural_to_natural(x, coset)
+
+    with ThreadPoolExecutor(8) as ex:
+        for got, want in ex.map(run, jobs):
+            eq(got, want)
+
+
 # -------------------------------------------------------------------- LDE
 
 @pytest.mark.parametrize("c,log_n,log_d", [(1, 0, 1), (2, 1, 1), (3, 3, 2), (5, 6, 3), (4, 12, 1), (3, 13, 2),

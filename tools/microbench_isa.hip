@@ -106,6 +106,26 @@ K32X(k_cnd_vcc_vv, E8(CNDVCC))
 #define XOR(i, j) "v_xor_b32 %" S(i) ", %" S(j) ", %" S(i) "\n"
 K32X(k_xor, E8(XOR))
 
+// 32-bit ALU candidates for BLAKE2s (rotate / xor / add forms)
+#define PERM(i, j) "v_perm_b32 %" S(i) ", %" S(i) ", %" S(i) ", %17\n"
+K32X(k_perm, E8(PERM))
+#define ALIGNBYTE(i, j) "v_alignbyte_b32 %" S(i) ", %" S(j) ", %" S(i) ", 2\n"
+K32X(k_alignbyte, E8(ALIGNBYTE))
+#define LSHLOR(i, j) "v_lshl_or_b32 %" S(i) ", %" S(i) ", 7, %" S(j) "\n"
+K32X(k_lshl_or, E8(LSHLOR))
+#define XAD(i, j) "v_xad_u32 %" S(i) ", %" S(i) ", %16, %" S(j) "\n"
+K32X(k_xad, E8(XAD))
+#define BITOP3(i, j) "v_bitop3_b32 %" S(i) ", %" S(i) ", %16, %" S(j) " bitop3:0x96\n"
+K32X(k_bitop3, E8(BITOP3))
+#define OR3(i, j) "v_or3_b32 %" S(i) ", %" S(i) ", %16, %" S(j) "\n"
+K32X(k_or3, E8(OR3))
+#define LSHLADD32(i, j) "v_lshl_add_u32 %" S(i) ", %" S(i) ", 3, %" S(j) "\n"
+K32X(k_lshl_add_u32, E8(LSHLADD32))
+#define PKADD16(i, j) "v_pk_add_u16 %" S(i) ", %" S(i) ", %16\n"
+K32X(k_pk_add_u16, E8(PKADD16))
+#define LSHR32(i, j) "v_lshrrev_b32 %" S(i) ", 7, %" S(i) "\n"
+K32X(k_lshr32, E8(LSHR32))
+
 int main() {
     const int blocks = 256 * 8, threads = 256;
     uint64_t* out;
@@ -131,6 +151,11 @@ int main() {
         {"v_mov_b32", k_mov, 16}, {"v_and_b32", k_and, 16}, {"v_xor_b32", k_xor, 16},
         {"v_cndmask_b32_e32 v,v,vcc", k_cnd_vcc_vv, 16},
         {"v_fma_f64", k_fma_f64, 16},           {"v_pk_fma_f32", k_pk_fma_f32, 16},
+        {"v_perm_b32", k_perm, 16},             {"v_alignbyte_b32", k_alignbyte, 16},
+        {"v_lshl_or_b32", k_lshl_or, 16},       {"v_xad_u32", k_xad, 16},
+        {"v_bitop3_b32", k_bitop3, 16},         {"v_or3_b32", k_or3, 16},
+        {"v_lshl_add_u32", k_lshl_add_u32, 16}, {"v_pk_add_u16", k_pk_add_u16, 16},
+        {"v_lshrrev_b32", k_lshr32, 16},
     };
     // clock: assume 2.4 GHz nominal; also report absolute ns
     for (auto& t : tests) {

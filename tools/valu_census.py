@@ -26,8 +26,11 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 LLVM = "/opt/rocm/lib/llvm/bin"
 HIPCC = "/opt/rocm/bin/hipcc"
 
-FULL_RATE = re.compile(r"^v_(add_u32|sub_u32|mov_b32|and_b32|or_b32|xor_b32|lshlrev_b32|lshrrev_b32|"
-                       r"alignbit_b32|bfe_u32|and_or_b32|or3_b32|xad_u32|not_b32|cndmask_b32_e32)")
+# full rate on gfx950 (profiles/r1_isa_rates.txt, r1n_isa_rates_alu32.txt): VOP2 32-bit add /
+# logic / shift / move and v_bitop3_b32; the VOP3-only 32-bit forms (v_add3, v_alignbit,
+# v_perm, v_lshl_or, v_xad, v_or3, ...) issue at half rate like the carry / 64-bit ops
+FULL_RATE = re.compile(r"^v_(add_u32_e32|sub_u32_e32|mov_b32|and_b32_e32|or_b32_e32|xor_b32_e32|lshlrev_b32_e32|"
+                       r"lshrrev_b32_e32|not_b32|bitop3_b32)")
 
 
 def disassemble(name="merkle"):
@@ -123,6 +126,39 @@ def ntt_census():
     return out
 
 
+def loop_census(instrs):
+    """(slots outside the single loop, slots of one loop iteration) of a kernel with one loop."""
+    base = instrs[0][0]
+    back = [(i, a, t) for i, (a, mn, t) in enumerate(instrs) if t is not None and base + t < a]
+    if not back:
+        raise SystemExit("no loop found")
+    # the loop is the widest backward edge; the others return from out-of-line blocks
+    spans = []
+    for i_end, a, t in back:
+        start = next(k for k, (aa, _, _) in enumerate(instrs) if aa == base + t)
+        spans.append((i_end - start, start, i_end))
+    _, start, i_end = max(spans)
+    out = body = 0
+    for k, (_, mn, _) in enumerate(instrs):
+        if not mn.startswith("v_"):
+            continue
+        cost = 1 if FULL_RATE.match(mn) else 2
+        if start <= k <= i_end:
+            body += cost
+        else:
+            out += cost
+    return out, body
+
+
+def blake2s_census():
+    """Issue slots of the Blake2s256 leaf kernel (b2s_leaf_kernel<false, true>): a leaf of C
+    columns (C % 8 == 0) runs the block loop C/8 - 1 times plus the final block outside it."""
+    dis = disassemble("blake2s")
+    ins = parse(kernel_lines(dis, "b2s_leaf_kernelILb0ELb1E"))
+    out, body = loop_census(ins)
+    return {"kernel": "b2s_leaf_kernel<false, true>", "slots_outside_loop": out, "slots_per_block": body}
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--json")
@@ -133,7 +169,8 @@ def main():
     res = {"kernel": "node_level_kernel (one Poseidon2 permutation per lane + 64 B in / 32 B out)",
            "valu_instr_per_perm": valu, "issue_slots_per_perm": slots,
            "top": dict(sorted(hist.items(), key=lambda kv: -kv[1])[:12]),
-           "ntt_ct": ntt_census()}
+           "ntt_ct": ntt_census(),
+           "blake2s": blake2s_census()}
     print(json.dumps(res, indent=1))
     if args.json:
         with open(args.json, "w") as f:
