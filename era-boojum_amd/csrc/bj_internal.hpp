@@ -64,13 +64,6 @@ hipError_t launch_fold_all(uint64_t* dst, size_t dst_col_stride, size_t dst_shar
                            size_t src_stride, uint32_t n_cols, uint32_t log_m, uint32_t log_f, uint32_t shards,
                            const uint64_t* s_pow_m, hipStream_t st);
 
-// ntt_fast.hip: register-resident passes for 2^18 <= n <= 2^23
-bool fast_ntt_supported(uint32_t log_n);
-hipError_t launch_dif_fast(uint64_t* dst, size_t dst_stride, const uint64_t* src, size_t src_stride, uint32_t n_cols,
-                           uint32_t log_n, const uint64_t* tw_pyr, bool canon_out, hipStream_t st);
-hipError_t launch_lde_forward_fast(uint64_t* lde, size_t lde_col_stride, uint32_t n_cosets, const uint64_t* raw,
-                                   size_t raw_stride, bool raw_bitrev, uint32_t n_cols, uint32_t log_n,
-                                   const uint64_t* tw_pyr, const uint64_t* pw, size_t pw_stride, hipStream_t st);
 }  // namespace bj
 
 namespace bj {

@@ -16,7 +16,7 @@
 // multiplies the stage-0 lower operands by n^-1 as well, so the inverse transform returns
 // the monomials themselves (utils.rs:295-304 after ifft's x n^-1), not n * monomials.
 //
-// Tiling is that of ntt_fast.hip. Each thread holds 32 elements in VGPRs and runs up to five
+// Tiling: each thread holds 32 elements in VGPRs and runs up to five
 // stages in registers; LDS (XOR-swizzled) only re-deals elements between register phases.
 // * head: the first R = log n - 13 stages on tiles of 2^R rows x 2^(13-R) adjacent columns.
 //   Stage v's group index is the row's top v bits, so in phase A' the twiddles are

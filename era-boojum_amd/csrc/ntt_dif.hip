@@ -308,8 +308,6 @@ int dif_plan(uint32_t log_n, uint32_t* Rs, uint32_t* u0s) {
 hipError_t launch_dif(uint64_t* dst, size_t dst_stride, const uint64_t* src, size_t src_stride, uint32_t n_cols,
                       uint32_t log_n, const uint64_t* tw_pyr, bool canon_out, hipStream_t st) {
     if (n_cols == 0) return hipSuccess;
-    if (fast_ntt_supported(log_n))
-        return launch_dif_fast(dst, dst_stride, src, src_stride, n_cols, log_n, tw_pyr, canon_out, st);
     uint32_t Rs[8], u0s[8];
     const int np = dif_plan(log_n, Rs, u0s);
     const uint64_t* cs = src;
@@ -333,9 +331,6 @@ hipError_t launch_lde_forward(uint64_t* lde, size_t lde_col_stride, uint32_t n_c
                               size_t raw_stride, bool raw_bitrev, uint32_t n_cols, uint32_t log_n,
                               const uint64_t* tw_pyr, const uint64_t* pw, size_t pw_stride, hipStream_t st) {
     if (n_cols == 0) return hipSuccess;
-    if (fast_ntt_supported(log_n) && lde_col_stride == ((size_t)n_cosets << log_n))
-        return launch_lde_forward_fast(lde, lde_col_stride, n_cosets, raw, raw_stride, raw_bitrev, n_cols, log_n,
-                                       tw_pyr, pw, pw_stride, st);
     uint32_t Rs[8], u0s[8];
     const int np = dif_plan(log_n, Rs, u0s);
     const size_t n = (size_t)1 << log_n;
