@@ -48,6 +48,11 @@ SIGNATURES = {
     "bj_blake2s_nodes_d": ([_vp, _sz, _u32, _vp, _vp], _int),
     "bj_blake2s_leaves_partial_d": ([_vp, _u32, _sz, _sz, _u64, _vp, _vp, _int, _vp], _int),
     "bj_blake2s_leaf_h": ([_u64p, _sz, _u64p], _int),
+    "bj_keccak256_leaves_d": ([_vp, _u32, _sz, _sz, _vp, _vp], _int),
+    "bj_keccak256_leaves_chunked_d": ([_vp, _u32, _sz, _sz, _u32, _vp, _vp], _int),
+    "bj_keccak256_nodes_d": ([_vp, _sz, _u32, _vp, _vp], _int),
+    "bj_keccak256_leaf_h": ([_u64p, _sz, _u64p], _int),
+    "bj_keccak256_node_h": ([_u64p, _u64p, _u64p], _int),
     "bj_blake2s_node_h": ([_u64p, _u64p, _u64p], _int),
     "bj_lde_commit_d": ([_vp, _u32, _sz, _u32, _u32, _u32, _vp, _vp, _vp, _vp, _u64p, _vp], _int),
     "bj_lde_commit_h": ([_u64p, _u32, _u32, _u32, _u32, _u64p, _u64p, _u64p, _u64p], _int),

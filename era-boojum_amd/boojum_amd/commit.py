@@ -48,7 +48,7 @@ def witness_commit(trace, lde_degree, cap_size, workspace=None, hasher="poseidon
     """Commit a (C, n) int64 CUDA trace tensor.  Returns the workspace holding
     lde (C, D, n), leaves, nodes and cap (all on device, canonical).
     Asynchronous on the current stream.  hasher: "poseidon2" (GoldilocksPoseidon2Sponge, the
-    recursive-mode tree) or "blake2s" (Blake2s256, the non-recursive one)."""
+    recursive-mode tree), "blake2s" (Blake2s256, the non-recursive one) or "keccak256"."""
     v, c, n, stride = col_view(trace)
     log_n, log_d = _log2(n), _log2(lde_degree)
     ws = workspace or CommitWorkspace(c, log_n, log_d, cap_size, device=v.device)
@@ -58,13 +58,15 @@ def witness_commit(trace, lde_degree, cap_size, workspace=None, hasher="poseidon
     if hasher == "poseidon2":
         call("bj_lde_commit_d", v.data_ptr(), c, stride, log_n, log_d, cap_size, ws.scratch.data_ptr(),
              ws.lde.data_ptr(), ws.leaves.data_ptr(), ws.nodes.data_ptr(), None, st)
-    elif hasher == "blake2s":
+    else:
+        from .merkle import HASHERS
+        if hasher not in HASHERS:
+            raise ValueError("unknown tree hasher %r" % (hasher,))
+        _, f_leaves, _, f_nodes = HASHERS[hasher]
         nl = n << log_d
         call("bj_lde_d", v.data_ptr(), c, stride, log_n, log_d, ws.scratch.data_ptr(), ws.lde.data_ptr(), st)
-        call("bj_blake2s_leaves_d", ws.lde.data_ptr(), c, nl, nl, ws.leaves.data_ptr(), st)
-        call("bj_blake2s_nodes_d", ws.leaves.data_ptr(), nl, cap_size, ws.nodes.data_ptr(), st)
-    else:
-        raise ValueError("unknown tree hasher %r" % (hasher,))
+        call(f_leaves, ws.lde.data_ptr(), c, nl, nl, ws.leaves.data_ptr(), st)
+        call(f_nodes, ws.leaves.data_ptr(), nl, cap_size, ws.nodes.data_ptr(), st)
     ws.hasher = hasher
     return ws
 

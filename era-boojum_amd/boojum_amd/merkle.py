@@ -1,11 +1,12 @@
-"""MerkleTreeWithCap / TreeHasher over the Poseidon2 Overwrite sponge or Blake2s256.
+"""MerkleTreeWithCap / TreeHasher over the Poseidon2 Overwrite sponge, Blake2s256 or Keccak256.
 
 Mirrors cs/oracle/merkle_tree.rs (construct :78-172, continue_from_leaf_hashes
 :388-449, get_cap :451-460, get_proof :462-480, verify_proof_over_cap :482-504) and the
 TreeHasher impls for GoldilocksPoseidon2Sponge<AbsorptionModeOverwrite>
 (cs/oracle/mod.rs:114-175; digests [u64; 4], canonical) and blake2::Blake2s256
-(:177-246; digests [u8; 32], held as 4 little-endian u64 words).  `hasher` selects one:
-"poseidon2" (the default, the recursive-mode tree) or "blake2s".
+(:179-245) and sha3::Keccak256 (:247-313), whose digests [u8; 32] are held as 4 little-endian
+u64 words.  `hasher` selects one: "poseidon2" (the default, the recursive-mode tree),
+"blake2s" (the non-recursive one) or "keccak256".
 
 Device layout: leaf_hashes (n_leaves, 4); node levels concatenated from the leaves up
 to the cap, (n_leaves - cap_size, 4) -- the reference's node_hashes_enumerated_from_leafs
@@ -74,10 +75,31 @@ class Blake2s256:
         return np.asarray(words, dtype=np.uint64).astype("<u8").tobytes()
 
 
+class Keccak256:
+    """TreeHasher<GoldilocksField> for sha3::Keccak256 (host-call forms), cs/oracle/mod.rs:247-313.
+    Digests are 32 bytes as 4 little-endian u64 words."""
+
+    @staticmethod
+    def hash_into_leaf(elements):
+        e = as_u64_host(elements)
+        out = np.zeros(4, dtype=np.uint64)
+        call("bj_keccak256_leaf_h", _hp(e) if e.size else None, e.size, _hp(out))
+        return out
+
+    @staticmethod
+    def hash_into_node(left, right, depth=0):
+        out = np.zeros(4, dtype=np.uint64)
+        call("bj_keccak256_node_h", _hp(as_u64_host(left)), _hp(as_u64_host(right)), _hp(out))
+        return out
+
+    digest_bytes = Blake2s256.digest_bytes
+
+
 # hasher name -> (host TreeHasher, leaves, chunked leaves, nodes entry points)
 HASHERS = {
     "poseidon2": (Poseidon2Sponge, "bj_merkle_leaves_d", "bj_merkle_leaves_chunked_d", "bj_merkle_nodes_d"),
     "blake2s": (Blake2s256, "bj_blake2s_leaves_d", "bj_blake2s_leaves_chunked_d", "bj_blake2s_nodes_d"),
+    "keccak256": (Keccak256, "bj_keccak256_leaves_d", "bj_keccak256_leaves_chunked_d", "bj_keccak256_nodes_d"),
 }
 
 

@@ -44,7 +44,7 @@ inline size_t pw_hi_len(uint32_t log_n) { return log_n > 12 ? ((size_t)1 << (log
 }  // namespace bj
 
 namespace bj {
-// blake2s.hip: Blake2s256 tree hasher (cs/oracle/mod.rs:177-246)
+// blake2s.hip: Blake2s256 tree hasher (cs/oracle/mod.rs:179-245)
 hipError_t launch_b2s_leaves(const uint64_t* src, size_t col_stride, uint32_t n_cols, size_t n_leaves,
                              uint64_t cols_before, const uint64_t* state_in, uint64_t* out, bool final_,
                              hipStream_t st);
@@ -53,6 +53,14 @@ hipError_t launch_b2s_leaves_chunked(const uint64_t* src, size_t col_stride, uin
 hipError_t launch_b2s_nodes(const uint64_t* leaves, size_t n_leaves, uint32_t cap_size, uint64_t* nodes,
                             hipStream_t st);
 hipError_t launch_b2s_words(const uint64_t* words, uint32_t n_words, uint64_t* out, hipStream_t st);
+
+// keccak.hip: Keccak256 tree hasher (cs/oracle/mod.rs:247-313)
+hipError_t launch_kc_leaves(const uint64_t* src, size_t col_stride, uint32_t n_cols, size_t n_leaves, uint64_t* out,
+                            hipStream_t st);
+hipError_t launch_kc_leaves_chunked(const uint64_t* src, size_t col_stride, uint32_t n_cols, uint32_t log_e,
+                                    size_t n_leaves, uint64_t* out, hipStream_t st);
+hipError_t launch_kc_nodes(const uint64_t* leaves, size_t n_leaves, uint32_t cap_size, uint64_t* nodes,
+                           hipStream_t st);
 
 // shard.hip: sub-coset fold of the bit-reversed coefficients (G > D shards)
 constexpr uint32_t kMaxFold = 64;

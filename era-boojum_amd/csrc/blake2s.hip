@@ -1,11 +1,11 @@
 // Blake2s256 tree hashing kernels (gfx950): the TreeHasher impl for blake2::Blake2s256
-// (cs/oracle/mod.rs:177-246), the tree hasher of the non-recursive prover configs
+// (cs/oracle/mod.rs:179-245), the tree hasher of the non-recursive prover configs
 // (gadgets/sha256/mod.rs:263-269).  Blake2s256 = BLAKE2s, 32-byte digest, no key (RFC 7693).
 //
-// Leaf (hash_into_leaf, :204-216): the message is the canonical little-endian bytes of the
+// Leaf (hash_into_leaf, :203-215): the message is the canonical little-endian bytes of the
 // leaf's elements, 8 elements = one 64-byte block; every block but the last is compressed
 // as more data follows, the last (zero-padded; one zero block for an empty leaf) carries
-// the final flag and the byte count.  Node (:233-245): one block, left || right, final,
+// the final flag and the byte count.  Node (:234-245): one block, left || right, final,
 // 64 bytes.  Digests are 32 bytes, held as 4 little-endian u64 words in the same (N, 4)
 // buffers as the Poseidon2 digests.
 //
@@ -83,7 +83,7 @@ __device__ __forceinline__ void init_h(uint32_t* h) {
     h[0] ^= 0x01010000u ^ 32u;  // parameter block: digest 32, no key, fanout 1, depth 1
 }
 
-// element -> two message words: as_u64_reduced().to_le_bytes() (cs/oracle/mod.rs:194-197)
+// element -> two message words: as_u64_reduced().to_le_bytes() (cs/oracle/mod.rs:190-193)
 __device__ __forceinline__ void put(uint32_t* m, int i, uint64_t v) {
     v = gl::canon(v);
     m[2 * i] = (uint32_t)v;

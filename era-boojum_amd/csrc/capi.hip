@@ -599,6 +599,32 @@ int bj_blake2s_nodes_d(const uint64_t* leaves, size_t n_leaves, uint32_t cap_siz
     return BJ_OK;
 }
 
+// ------------------------------------------------------------ Keccak256 trees
+
+int bj_keccak256_leaves_d(const uint64_t* src, uint32_t n_cols, size_t col_stride, size_t n_leaves, uint64_t* leaves,
+                          void* stream) {
+    HIP_TRY(bj::launch_kc_leaves(src, col_stride, n_cols, n_leaves, leaves, S(stream)), "leaves");
+    return BJ_OK;
+}
+
+int bj_keccak256_leaves_chunked_d(const uint64_t* src, uint32_t n_cols, size_t col_stride, size_t n_leaves,
+                                  uint32_t elems_per_leaf, uint64_t* out, void* stream) {
+    if (!is_pow2(elems_per_leaf)) return fail(BJ_EINVAL, "elements_to_take_per_leaf must be a power of two");
+    uint32_t log_e = 0;
+    while ((1u << log_e) < elems_per_leaf) log_e++;
+    if ((uint64_t)n_cols << log_e > 0xFFFFFFFFull) return fail(BJ_EINVAL, "leaf too long");
+    HIP_TRY(bj::launch_kc_leaves_chunked(src, col_stride, n_cols, log_e, n_leaves, out, S(stream)), "leaves");
+    return BJ_OK;
+}
+
+int bj_keccak256_nodes_d(const uint64_t* leaves, size_t n_leaves, uint32_t cap_size, uint64_t* nodes,
+                         void* stream) {
+    if (!is_pow2(n_leaves) || !is_pow2(cap_size) || n_leaves <= cap_size)
+        return fail(BJ_EINVAL, "need power-of-two n_leaves > cap_size (merkle_tree.rs:83-96)");
+    HIP_TRY(bj::launch_kc_nodes(leaves, n_leaves, cap_size, nodes, S(stream)), "nodes");
+    return BJ_OK;
+}
+
 int bj_lde_commit_d(const uint64_t* trace, uint32_t n_cols, size_t trace_stride, uint32_t log_n, uint32_t log_lde,
                     uint32_t cap_size, uint64_t* scratch, uint64_t* lde, uint64_t* leaves, uint64_t* nodes,
                     uint64_t* cap_h, void* stream) {
@@ -698,6 +724,28 @@ int bj_blake2s_node_h(const uint64_t* left4, const uint64_t* right4, uint64_t* o
     HIP_TRY(hipMemcpy(d.p, left4, 32, hipMemcpyHostToDevice), "memcpy");
     HIP_TRY(hipMemcpy(d.p + 4, right4, 32, hipMemcpyHostToDevice), "memcpy");
     if (int r = bj_blake2s_nodes_d(d.p, 2, 1, d.p + 8, nullptr)) return r;
+    HIP_TRY(hipMemcpy(out4, d.p + 8, 32, hipMemcpyDeviceToHost), "memcpy");
+    return BJ_OK;
+}
+
+int bj_keccak256_leaf_h(const uint64_t* elems, size_t n_elems, uint64_t* out4) {
+    if (n_elems > 0xFFFFFFFFull) return fail(BJ_EINVAL, "leaf too long");
+    DBuf d, o;
+    HIP_TRY(hipMalloc(&d.p, (n_elems ? n_elems : 1) * 8), "hipMalloc");
+    HIP_TRY(hipMalloc(&o.p, 32), "hipMalloc");
+    if (n_elems) HIP_TRY(hipMemcpy(d.p, elems, n_elems * 8, hipMemcpyHostToDevice), "memcpy");
+    // the elements as n_elems one-row columns of one leaf
+    HIP_TRY(bj::launch_kc_leaves(d.p, 1, (uint32_t)n_elems, 1, o.p, nullptr), "keccak256");
+    HIP_TRY(hipMemcpy(out4, o.p, 32, hipMemcpyDeviceToHost), "memcpy");
+    return BJ_OK;
+}
+
+int bj_keccak256_node_h(const uint64_t* left4, const uint64_t* right4, uint64_t* out4) {
+    DBuf d;
+    HIP_TRY(hipMalloc(&d.p, 96), "hipMalloc");
+    HIP_TRY(hipMemcpy(d.p, left4, 32, hipMemcpyHostToDevice), "memcpy");
+    HIP_TRY(hipMemcpy(d.p + 4, right4, 32, hipMemcpyHostToDevice), "memcpy");
+    if (int r = bj_keccak256_nodes_d(d.p, 2, 1, d.p + 8, nullptr)) return r;
     HIP_TRY(hipMemcpy(out4, d.p + 8, 32, hipMemcpyDeviceToHost), "memcpy");
     return BJ_OK;
 }

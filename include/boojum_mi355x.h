@@ -190,7 +190,7 @@ int bj_merkle_nodes_d(const uint64_t* leaves, size_t n_leaves, uint32_t cap_size
 
 /* ------------------------------------------------ Blake2s256 tree hasher */
 /* MerkleTreeWithCap<GoldilocksField, blake2::Blake2s256>: the TreeHasher impl of
- * cs/oracle/mod.rs:177-246, used by the non-recursive prover configs
+ * cs/oracle/mod.rs:179-245, used by the non-recursive prover configs
  * (gadgets/sha256/mod.rs:263-269).  Leaf = BLAKE2s-256 (RFC 7693, no key) of the canonical
  * little-endian bytes of the leaf's elements (as_u64_reduced().to_le_bytes(), :194-197);
  * node = BLAKE2s-256(left || right) (:233-245).  A digest is 32 bytes, stored as 4
@@ -213,6 +213,21 @@ int bj_blake2s_leaves_partial_d(const uint64_t* src, uint32_t n_cols, size_t col
 /* host seams (TreeHasher::hash_into_leaf / hash_into_node) */
 int bj_blake2s_leaf_h(const uint64_t* elems, size_t n_elems, uint64_t* out4);
 int bj_blake2s_node_h(const uint64_t* left4, const uint64_t* right4, uint64_t* out4);
+
+/* ---------------------------------------------- Keccak256 tree hasher */
+/* MerkleTreeWithCap<GoldilocksField, sha3::Keccak256>: the TreeHasher impl of
+ * cs/oracle/mod.rs:247-313.  Leaf = Keccak256 (rate 136 bytes, domain byte 0x01) of the
+ * canonical little-endian bytes of the leaf's elements; node = Keccak256(left || right).
+ * Digests are 32 bytes as 4 little-endian u64 words.  Same arguments, layouts and
+ * preconditions as the bj_merkle_* calls. */
+int bj_keccak256_leaves_d(const uint64_t* src, uint32_t n_cols, size_t col_stride, size_t n_leaves,
+                          uint64_t* leaves, void* stream);
+int bj_keccak256_leaves_chunked_d(const uint64_t* src, uint32_t n_cols, size_t col_stride, size_t n_leaves,
+                                  uint32_t elems_per_leaf, uint64_t* out, void* stream);
+int bj_keccak256_nodes_d(const uint64_t* leaves, size_t n_leaves, uint32_t cap_size, uint64_t* nodes,
+                         void* stream);
+int bj_keccak256_leaf_h(const uint64_t* elems, size_t n_elems, uint64_t* out4);
+int bj_keccak256_node_h(const uint64_t* left4, const uint64_t* right4, uint64_t* out4);
 
 /* ------------------------------------------------------- whole commitment */
 

@@ -368,12 +368,12 @@ void bjo_hash_into_node(const u64* l, const u64* r, u64* out4) {
 
 /* ------------------------------------------- Blake2s256 tree hasher (a18') */
 
-/* TreeHasher for blake2::Blake2s256 (cs/oracle/mod.rs:177-246), the tree hasher of the
+/* TreeHasher for blake2::Blake2s256 (cs/oracle/mod.rs:179-245), the tree hasher of the
  * non-recursive prover configs (gadgets/sha256/mod.rs:263-269).  Third-party crate
  * blake2 = "0.10" (Cargo.toml:23, resolved 0.10.6): Blake2s256 = BLAKE2s with a 32-byte
  * digest, no key, salt or personalisation, i.e. RFC 7693 (restated below).
- *   leaf: update(as_u64_reduced(x).to_le_bytes()) for each element, finalize (:187-231);
- *   node: update(left 32 B), update(right 32 B), finalize (:233-245).
+ *   leaf: update(as_u64_reduced(x).to_le_bytes()) for each element, finalize (:190-231);
+ *   node: update(left 32 B), update(right 32 B), finalize (:234-245).
  * Digests are 32 bytes, stored here as 4 little-endian u64 words. */
 static const uint32_t B2S_IV[8] = {0x6A09E667u, 0xBB67AE85u, 0x3C6EF372u, 0xA54FF53Au,
                                    0x510E527Fu, 0x9B05688Cu, 0x1F83D9ABu, 0x5BE0CD19u};
@@ -465,9 +465,95 @@ void bjo_blake2s_node(const u64* l, const u64* r, u64* out4) {
     bjo_blake2s(buf, 64, (uint8_t*)out4);
 }
 
+/* ------------------------------------------- Keccak256 tree hasher (a18'') */
+
+/* TreeHasher for sha3::Keccak256 (cs/oracle/mod.rs:247-313).  Third-party crate sha3 (git
+ * RustCrypto/hashes rev 7a187e93, Cargo.toml:15): Keccak256 = Keccak[c = 512] with the
+ * original Keccak padding (pad10*1 with domain byte 0x01), 32-byte digest; restated from the
+ * Keccak reference (FIPS 202 section 3 permutation, rate 136 bytes).  The same sponge with
+ * domain byte 0x06 is SHA3-256, which pins the permutation against hashlib.sha3_256.
+ *   leaf: update(as_u64_reduced(x).to_le_bytes()) per element, finalize (:258-299);
+ *   node: update(left 32 B), update(right 32 B), finalize (:302-313). */
+static const u64 KECCAK_RC[24] = {
+    0x0000000000000001ULL, 0x0000000000008082ULL, 0x800000000000808AULL, 0x8000000080008000ULL,
+    0x000000000000808BULL, 0x0000000080000001ULL, 0x8000000080008081ULL, 0x8000000000008009ULL,
+    0x000000000000008AULL, 0x0000000000000088ULL, 0x0000000080008009ULL, 0x000000008000000AULL,
+    0x000000008000808BULL, 0x800000000000008BULL, 0x8000000000008089ULL, 0x8000000000008003ULL,
+    0x8000000000008002ULL, 0x8000000000000080ULL, 0x000000000000800AULL, 0x800000008000000AULL,
+    0x8000000080008081ULL, 0x8000000000008080ULL, 0x0000000080000001ULL, 0x8000000080008008ULL};
+/* rho offsets r[x + 5 y] */
+static const int KECCAK_RHO[25] = {0, 1, 62, 28, 27, 36, 44, 6, 55, 20, 3, 10, 43,
+                                   25, 39, 41, 45, 15, 21, 8, 18, 2, 61, 56, 14};
+
+static inline u64 rotl64(u64 x, int r) { return r ? (x << r) | (x >> (64 - r)) : x; }
+
+/* Keccak-f[1600], lanes A[x + 5 y] (FIPS 202 3.2: theta, rho, pi, chi, iota) */
+void bjo_keccak_f1600(u64* A) {
+    for (int round = 0; round < 24; round++) {
+        u64 C[5], D[5], B[25];
+        for (int x = 0; x < 5; x++) C[x] = A[x] ^ A[x + 5] ^ A[x + 10] ^ A[x + 15] ^ A[x + 20];
+        for (int x = 0; x < 5; x++) D[x] = C[(x + 4) % 5] ^ rotl64(C[(x + 1) % 5], 1);
+        for (int i = 0; i < 25; i++) A[i] ^= D[i % 5];
+        for (int x = 0; x < 5; x++)
+            for (int y = 0; y < 5; y++) B[y + 5 * ((2 * x + 3 * y) % 5)] = rotl64(A[x + 5 * y], KECCAK_RHO[x + 5 * y]);
+        for (int x = 0; x < 5; x++)
+            for (int y = 0; y < 5; y++)
+                A[x + 5 * y] = B[x + 5 * y] ^ (~B[(x + 1) % 5 + 5 * y] & B[(x + 2) % 5 + 5 * y]);
+        A[0] ^= KECCAK_RC[round];
+    }
+}
+
+/* sponge with rate 136 bytes, 32-byte output; domain 0x01 = Keccak256, 0x06 = SHA3-256 */
+void bjo_keccak256(const uint8_t* data, size_t len, uint8_t* out32, int domain) {
+    u64 A[25] = {0};
+    uint8_t block[136];
+    size_t off = 0;
+    for (;;) {
+        size_t take = len - off < 136 ? len - off : 136;
+        int last = take < 136;
+        memset(block, 0, sizeof(block));
+        memcpy(block, data + off, take);
+        off += take;
+        if (last) {
+            block[take] ^= (uint8_t)domain;
+            block[135] ^= 0x80;
+        }
+        for (int i = 0; i < 17; i++) {
+            u64 w = 0;
+            for (int b = 0; b < 8; b++) w |= (u64)block[8 * i + b] << (8 * b);
+            A[i] ^= w;
+        }
+        bjo_keccak_f1600(A);
+        if (last) break;
+    }
+    for (int i = 0; i < 4; i++)
+        for (int b = 0; b < 8; b++) out32[8 * i + b] = (uint8_t)(A[i] >> (8 * b));
+}
+
+static void keccak_leaf_strided(const u64* elems, size_t count, size_t stride, u64* out4) {
+    uint8_t stackbuf[8 * 64] = {0};
+    uint8_t* buf = count <= 64 ? stackbuf : (uint8_t*)malloc(8 * count);
+    for (size_t i = 0; i < count; i++) {
+        u64 v = gl_canon(elems[i * stride]);
+        for (int b = 0; b < 8; b++) buf[8 * i + b] = (uint8_t)(v >> (8 * b));
+    }
+    bjo_keccak256(buf, 8 * count, (uint8_t*)out4, 0x01);
+    if (buf != stackbuf) free(buf);
+}
+
+void bjo_keccak_leaf(const u64* elems, size_t count, u64* out4) { keccak_leaf_strided(elems, count, 1, out4); }
+
+void bjo_keccak_node(const u64* l, const u64* r, u64* out4) {
+    uint8_t buf[64];
+    memcpy(buf, l, 32);
+    memcpy(buf + 32, r, 32);
+    bjo_keccak256(buf, 64, (uint8_t*)out4, 0x01);
+}
+
 /* ------------------------------------------------------------ Merkle (a19) */
 
-/* tree hashers: 0 = GoldilocksPoseidon2Sponge<AbsorptionModeOverwrite>, 1 = Blake2s256 */
+/* tree hashers: 0 = GoldilocksPoseidon2Sponge<AbsorptionModeOverwrite>, 1 = Blake2s256,
+ * 2 = Keccak256 */
 typedef struct {
     const u64* lde; size_t col_stride; uint32_t n_cols; u64* leaves;
     const u64* prev; u64* next; int hasher;
@@ -475,6 +561,7 @@ typedef struct {
 
 static void hash_node_h(int hasher, const u64* l, const u64* r, u64* out4) {
     if (hasher == 1) bjo_blake2s_node(l, r, out4);
+    else if (hasher == 2) bjo_keccak_node(l, r, out4);
     else bjo_hash_into_node(l, r, out4);
 }
 
@@ -482,6 +569,7 @@ static void leaf_job(void* c, size_t b, size_t e) {
     mk_ctx_t* x = (mk_ctx_t*)c;
     for (size_t L = b; L < e; L++) {
         if (x->hasher == 1) b2s_leaf_strided(x->lde + L, x->n_cols, x->col_stride, x->leaves + 4 * L);
+        else if (x->hasher == 2) keccak_leaf_strided(x->lde + L, x->n_cols, x->col_stride, x->leaves + 4 * L);
         else leaf_hash_strided(x->lde + L, x->n_cols, x->col_stride, x->leaves + 4 * L);
     }
 }

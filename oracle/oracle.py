@@ -54,6 +54,9 @@ def lib():
         L.bjo_blake2s.argtypes = [ctypes.c_char_p, sz, ctypes.c_char_p]
         L.bjo_blake2s_leaf.argtypes = [_u64p, sz, _u64p]
         L.bjo_blake2s_node.argtypes = [_u64p, _u64p, _u64p]
+        L.bjo_keccak256.argtypes = [ctypes.c_char_p, sz, ctypes.c_char_p, i]
+        L.bjo_keccak_leaf.argtypes = [_u64p, sz, _u64p]
+        L.bjo_keccak_node.argtypes = [_u64p, _u64p, _u64p]
         L.bjo_merkle_construct_with.restype = i
         L.bjo_merkle_construct_with.argtypes = [_u64p, sz, u32, sz, u32, _u64p, _u64p, i, i]
         L.bjo_verify_proof_over_cap_with.restype = i
@@ -175,7 +178,7 @@ def hash_into_node(left, right):
     return out
 
 
-HASHERS = {"poseidon2": 0, "blake2s": 1}
+HASHERS = {"poseidon2": 0, "blake2s": 1, "keccak256": 2}
 
 
 def blake2s(data):
@@ -187,7 +190,7 @@ def blake2s(data):
 
 
 def blake2s_leaf(elems):
-    """TreeHasher::hash_into_leaf for Blake2s256 (cs/oracle/mod.rs:204-216): the canonical
+    """TreeHasher::hash_into_leaf for Blake2s256 (cs/oracle/mod.rs:203-215): the canonical
     little-endian bytes of each element.  Digest as 4 little-endian u64 words."""
     e = _u64(elems)
     n = e.size
@@ -199,9 +202,35 @@ def blake2s_leaf(elems):
 
 
 def blake2s_node(left, right):
-    """TreeHasher::hash_into_node for Blake2s256 (cs/oracle/mod.rs:233-245)."""
+    """TreeHasher::hash_into_node for Blake2s256 (cs/oracle/mod.rs:234-245)."""
     out = np.zeros(4, dtype=np.uint64)
     lib().bjo_blake2s_node(_p(_u64(left)), _p(_u64(right)), _p(out))
+    return out
+
+
+def keccak256(data, domain=0x01):
+    """Keccak256 (domain 0x01, the sha3 crate's Keccak256) or SHA3-256 (domain 0x06) of bytes."""
+    data = bytes(data)
+    out = ctypes.create_string_buffer(32)
+    lib().bjo_keccak256(data, len(data), out, domain)
+    return out.raw
+
+
+def keccak_leaf(elems):
+    """TreeHasher::hash_into_leaf for Keccak256 (cs/oracle/mod.rs:271-283)."""
+    e = _u64(elems)
+    n = e.size
+    if n == 0:
+        e = np.zeros(1, np.uint64)
+    out = np.zeros(4, dtype=np.uint64)
+    lib().bjo_keccak_leaf(_p(e), n, _p(out))
+    return out
+
+
+def keccak_node(left, right):
+    """TreeHasher::hash_into_node for Keccak256 (cs/oracle/mod.rs:302-313)."""
+    out = np.zeros(4, dtype=np.uint64)
+    lib().bjo_keccak_node(_p(_u64(left)), _p(_u64(right)), _p(out))
     return out
 
 

@@ -1,4 +1,4 @@
-"""GPU parity of the Blake2s256 tree hasher (csrc/blake2s.hip, cs/oracle/mod.rs:177-246),
+"""GPU parity of the Blake2s256 tree hasher (csrc/blake2s.hip, cs/oracle/mod.rs:179-245),
 the tree of the non-recursive prover configs (C5: gadgets/sha256/mod.rs:263-269), against the
 oracle (itself pinned to hashlib.blake2s, tests/test_oracle_blake2s.py): leaves of every
 block-padding case, non-canonical inputs, node levels to caps of 1..2048, chunked (FRI)

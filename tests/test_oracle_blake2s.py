@@ -1,5 +1,5 @@
 """The oracle's Blake2s256 tree hasher (oracle/boojum_oracle.c, restating RFC 7693 and the
-TreeHasher impl of cs/oracle/mod.rs:177-246) pinned against an independent implementation:
+TreeHasher impl of cs/oracle/mod.rs:179-245) pinned against an independent implementation:
 CPython's hashlib.blake2s (the BLAKE2 authors' reference code), plus the RFC 7693 Appendix B
 vector.  The reference's own dependency (blake2 = "0.10", Cargo.toml:23) is a third-party
 crate absent here; Blake2s256 is BLAKE2s-256 with no key, which hashlib.blake2s() is."""
