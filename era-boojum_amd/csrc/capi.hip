@@ -361,8 +361,8 @@ int bj_distribute_powers_d(uint64_t* cols, uint32_t n_cols, size_t col_stride, u
     return BJ_OK;
 }
 
-// Large sizes (2^18..2^23) run the coset-folded CT network of ntt_ct.hip, the shift folded
-// into its twiddle table; other sizes a DIF network (ntt_dif.hip) over its own cached twiddle
+// Sizes 2^13..2^23 run the coset-folded CT network of ntt_ct.hip, the shift folded
+// into its twiddle table; smaller ones a DIF network (ntt_dif.hip) over its own cached twiddle
 // pyramid. A twiddle pointer in the reference's format is accepted for signature parity and
 // not read.
 int bj_fft_natural_to_bitreversed_d(uint64_t* cols, uint32_t n_cols, size_t col_stride, uint32_t log_n,

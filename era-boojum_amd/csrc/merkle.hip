@@ -9,7 +9,7 @@
 //
 // Node: hash_into_node (cs/oracle/mod.rs:162-168) = permute([l, r, 0,0,0,0])[0..4], one
 // node per lane, level by level (continue_from_leaf_hashes, merkle_tree.rs:388-449);
-// the last levels (<= 2048 nodes) run in one workgroup through LDS.
+// the last levels (<= 256 nodes) run in one workgroup through LDS.
 #include <hip/hip_runtime.h>
 #include "gl.hpp"
 #include "poseidon2.hpp"
@@ -163,7 +163,8 @@ __global__ __launch_bounds__(256) void node_level_kernel(const uint64_t* __restr
     node_hash(lr, lr + 4, next + 4 * i);
 }
 
-// Remaining levels from `len` digests (len <= 4096) down to cap_size, one workgroup.
+// Remaining levels from `len` digests (len <= 4096; launch_nodes hands over len <= 512) down to
+// cap_size, one workgroup.
 __global__ __launch_bounds__(256) void node_tail_kernel(const uint64_t* __restrict__ prev, uint64_t* next,
                                                         uint32_t len, uint32_t cap_size) {
     __shared__ uint64_t buf[2][2048 * 4];
@@ -244,7 +245,10 @@ hipError_t launch_nodes(const uint64_t* leaves, size_t n_leaves, uint32_t cap_si
     const uint64_t* prev = leaves;
     uint64_t* out = nodes;
     size_t len = n_leaves;
-    while (len > cap_size && len > 4096) {
+    // every level above 512 digests as its own grid: a level costs one permutation's latency
+    // (~20 us at one wave per SIMD) when every lane hashes one node, while one workgroup
+    // would run a 2048-node level as 8 permutations in sequence
+    while (len > cap_size && len > 512) {
         size_t m = len / 2;
         hipLaunchKernelGGL(node_level_kernel, dim3((unsigned)((m + 255) / 256)), dim3(256), 0, st, prev, out, m);
         prev = out;

@@ -1,4 +1,4 @@
-// Coset-folded Cooley-Tukey NTT passes for the large sizes (2^18 <= n <= 2^23).
+// Coset-folded Cooley-Tukey NTT passes for 2^13 <= n <= 2^23.
 //
 // The reference's transform is serial_ct_ntt_natural_to_bitreversed (fft/mod.rs:659-734):
 // at the stage with 2^u groups, group k pairs (j, j + h) and does
@@ -138,19 +138,34 @@ __device__ __forceinline__ void head_b_stage(uint64_t* x, const uint64_t* __rest
     }
 }
 
+// Block -> (coset, unit = column * tiles + tile). XCD-aware when the unit count is a multiple
+// of 8: blocks are dealt round-robin over the 8 XCDs, so the n_cosets blocks of one unit sit
+// at ids unit8 + 8 c within a run of 8 n_cosets ids and share an XCD (its L2) and a time
+// window. Otherwise (small heads: few columns x 2^R tiles) the cosets of a unit are
+// consecutive ids. Speed only: any placement gives the same result.
+__device__ __forceinline__ void head_unit(uint32_t bid, uint32_t n_cosets, bool xcd, uint32_t& coset,
+                                          uint32_t& unit) {
+    if (xcd) {
+        const uint32_t rest = bid >> 3;
+        coset = rest % n_cosets;
+        unit = ((rest / n_cosets) << 3) | (bid & 7);
+    } else {
+        coset = bid % n_cosets;
+        unit = bid / n_cosets;
+    }
+}
+
 // MODE 0: natural source; MODE 1: bit-reversed source gathered in runs of 2^R words.
 // KAPPA: multiply the stage-0 lower operands by kappa (the inverse table's CT[1] already
 // carries it for the upper ones), i.e. scale the whole transform by kappa.
-// Grid: one dimension, XCD-aware.  Blocks are dealt round-robin over the 8 XCDs, so the
-// n_cosets blocks of one (column, tile) unit sit at ids unit8 + 8 c within a run of 8 n_cosets
-// ids: they share an XCD (its L2) and run at about the same time, so the source tile is
-// fetched from HBM once and re-read from L2 by the other cosets (speed only; any placement
-// gives the same result).
+// Grid: one dimension (head_unit): with the XCD-aware placement the source tile is fetched
+// from HBM once and re-read from L2 by the other cosets.
 template <int R, int MODE, bool KAPPA>
 __global__ __launch_bounds__(NT, 2) void ct_head_kernel(uint64_t* dst, size_t dst_col_stride, size_t coset_stride,
                                                         const uint64_t* src, size_t src_stride, uint32_t log_n,
                                                         const uint64_t* __restrict__ tab, size_t tab_stride,
-                                                        uint64_t kappa, uint32_t n_cosets, uint32_t log_tiles) {
+                                                        uint64_t kappa, uint32_t n_cosets, uint32_t log_tiles,
+                                                        int xcd) {
     constexpr int LOGW = 13 - R;
     constexpr uint32_t W = 1u << LOGW;
     constexpr uint32_t T = 1u << (R - 5);
@@ -158,10 +173,8 @@ __global__ __launch_bounds__(NT, 2) void ct_head_kernel(uint64_t* dst, size_t ds
     const uint32_t tid = threadIdx.x;
     const size_t n = (size_t)1 << log_n;
     const size_t S = n >> R;
-    const uint32_t bid = blockIdx.x;
-    const uint32_t rest = bid >> 3;
-    const uint32_t coset = rest % n_cosets;
-    const uint32_t unit = ((rest / n_cosets) << 3) | (bid & 7);
+    uint32_t coset, unit;
+    head_unit(blockIdx.x, n_cosets, xcd != 0, coset, unit);
     const uint32_t col = unit >> log_tiles;
     const size_t o0 = (size_t)(unit & ((1u << log_tiles) - 1)) * W;
     const uint64_t* sc = src + (size_t)col * src_stride;
@@ -212,6 +225,86 @@ __global__ __launch_bounds__(NT, 2) void ct_head_kernel(uint64_t* dst, size_t ds
     uint64_t* dc = dst + (size_t)col * dst_col_stride + (size_t)coset * coset_stride;
 #pragma unroll
     for (int k = 0; k < PT; k++) dc[(size_t)(32 * s + k) * S + o] = x[k];
+}
+
+// --------------------------------------------------------- small heads (R <= 4)
+
+// 2^13 <= n <= 2^17: the head's R = log n - 13 stages fit in registers. A tile is 2^R rows
+// x 2^(13-R) columns as above, and each thread holds all 2^R rows of C = 2^(5-R) columns
+// (columns t + 256 i), so every butterfly is thread-local and needs no LDS; the group index
+// of stage v is the row's top v bits, a compile-time register property, so every twiddle is
+// a wave-uniform (scalar) load. R = 0 (n = 2^13) is the load / gather / kappa step alone.
+// x[r * C + i] holds row r of column i; the pairs of stage v are (r, r + 2^(R-1-v)), i.e.
+// registers k and k + 2^(R-1-v) C.
+template <int R, int V>
+__device__ __forceinline__ void tw_ct_small(uint64_t* w, const uint64_t* __restrict__ ct) {
+    constexpr int C = 32 >> R;
+    constexpr int HK = (1 << (R - 1 - V)) * C;
+#pragma unroll
+    for (int q = 0; q < 16; q++) w[q] = ct[(1 << V) + ((pair_lo(q, HK) / C) >> (R - V))];
+}
+
+template <int R, int V>
+__device__ __forceinline__ void small_stage(uint64_t* x, const uint64_t* __restrict__ ct) {
+    if constexpr (V < R) {
+        uint64_t w[16];
+        tw_ct_small<R, V>(w, ct);
+        ct_stage<(1 << (R - 1 - V)) * (32 >> R)>(x, w);
+        small_stage<R, V + 1>(x, ct);
+    }
+}
+
+template <int R, int MODE, bool KAPPA>
+__global__ __launch_bounds__(NT, 2) void ct_head_small_kernel(uint64_t* dst, size_t dst_col_stride,
+                                                              size_t coset_stride, const uint64_t* src,
+                                                              size_t src_stride, uint32_t log_n,
+                                                              const uint64_t* __restrict__ tab, size_t tab_stride,
+                                                              uint64_t kappa, uint32_t n_cosets, uint32_t log_tiles,
+                                                              int xcd) {
+    constexpr int C = 32 >> R;          // columns per thread
+    constexpr uint32_t W = 1u << (13 - R);
+    const uint32_t t = threadIdx.x;
+    const size_t S = (size_t)1 << (log_n - R);
+    uint32_t coset, unit;
+    head_unit(blockIdx.x, n_cosets, xcd != 0, coset, unit);
+    const uint32_t col = unit >> log_tiles;
+    const size_t o0 = (size_t)(unit & ((1u << log_tiles) - 1)) * W;
+    const uint64_t* sc = src + (size_t)col * src_stride;
+    const uint64_t* ct = tab + (size_t)coset * tab_stride;
+    uint64_t x[PT];
+#pragma unroll
+    for (int i = 0; i < C; i++) {
+        const size_t o = o0 + t + NT * i;
+        if constexpr (MODE == 0) {
+#pragma unroll
+            for (int r = 0; r < (1 << R); r++) x[r * C + i] = sc[r * S + o];
+        } else {
+            // c_j at bitrev_n(j), j = r S + o: the 2^R rows of column o are one contiguous run
+            const size_t run = (size_t)gl::bitrev32((uint32_t)o, log_n - R) << R;
+#pragma unroll
+            for (int r = 0; r < (1 << R); r++) x[r * C + i] = sc[run + gl::bitrev32(r, R)];
+        }
+    }
+    if constexpr (KAPPA) {
+        if constexpr (R == 0) {
+            // stage 0 is the tail's: its lower operands are the first half of the column
+#pragma unroll
+            for (int i = 0; i < C; i++)
+                if (o0 + t + NT * i < (S >> 1)) x[i] = gl::mul(x[i], kappa);
+        } else {
+            // stage-0 lower operands: rows below 2^(R-1), registers 0..15
+#pragma unroll
+            for (int k = 0; k < 16; k += 4) mul4_by(x[k], x[k + 1], x[k + 2], x[k + 3], kappa);
+        }
+    }
+    small_stage<R, 0>(x, ct);
+    uint64_t* dc = dst + (size_t)col * dst_col_stride + (size_t)coset * coset_stride;
+#pragma unroll
+    for (int i = 0; i < C; i++) {
+        const size_t o = o0 + t + NT * i;
+#pragma unroll
+        for (int r = 0; r < (1 << R); r++) dc[r * S + o] = x[r * C + i];
+    }
 }
 
 // ------------------------------------------------------------------- tail
@@ -344,9 +437,14 @@ void launch_head_R(int mode, bool kappa_on, dim3 g, uint64_t* dst, size_t dst_co
                    uint64_t kappa, hipStream_t st) {
     const uint32_t log_tiles = log_n - 13;
     const dim3 g1(g.x * g.y * g.z);
-#define BJ_CT_HEAD(M, K)                                                                                         \
-    hipLaunchKernelGGL((ct_head_kernel<R, M, K>), g1, dim3(NT), 0, st, dst, dst_col_stride, coset_stride, src, \
-                       src_stride, log_n, tab, tab_stride, kappa, g.z, log_tiles)
+    const int xcd = ((g.x * g.y) % 8) == 0 ? 1 : 0;  // units (column x tile) in whole runs of 8
+#define BJ_CT_HEAD(M, K)                                                                                      \
+    if constexpr (R >= 5)                                                                                     \
+        hipLaunchKernelGGL((ct_head_kernel<R, M, K>), g1, dim3(NT), 0, st, dst, dst_col_stride, coset_stride, \
+                           src, src_stride, log_n, tab, tab_stride, kappa, g.z, log_tiles, xcd);             \
+    else                                                                                                      \
+        hipLaunchKernelGGL((ct_head_small_kernel<R, M, K>), g1, dim3(NT), 0, st, dst, dst_col_stride,         \
+                           coset_stride, src, src_stride, log_n, tab, tab_stride, kappa, g.z, log_tiles, xcd)
     if (mode == 0) {
         if (kappa_on) BJ_CT_HEAD(0, true);
         else BJ_CT_HEAD(0, false);
@@ -359,7 +457,7 @@ void launch_head_R(int mode, bool kappa_on, dim3 g, uint64_t* dst, size_t dst_co
 
 }  // namespace
 
-bool ct_ntt_supported(uint32_t log_n) { return log_n >= 18 && log_n <= 23; }
+bool ct_ntt_supported(uint32_t log_n) { return log_n >= 13 && log_n <= 23; }
 
 hipError_t launch_ct_table(uint64_t* out, uint32_t log_n, bool inverse, uint64_t shift, uint64_t scale1,
                            hipStream_t st) {
@@ -399,6 +497,11 @@ hipError_t launch_ct(uint64_t* dst, size_t dst_col_stride, size_t coset_stride, 
     const int mode = src_bitrev ? 1 : 0;
     const bool k_on = kappa != 0;
     switch (log_n - 13) {
+        case 0: launch_head_R<0>(mode, k_on, g, dst, dst_col_stride, coset_stride, src, src_stride, log_n, tab, tab_stride, kappa, st); break;
+        case 1: launch_head_R<1>(mode, k_on, g, dst, dst_col_stride, coset_stride, src, src_stride, log_n, tab, tab_stride, kappa, st); break;
+        case 2: launch_head_R<2>(mode, k_on, g, dst, dst_col_stride, coset_stride, src, src_stride, log_n, tab, tab_stride, kappa, st); break;
+        case 3: launch_head_R<3>(mode, k_on, g, dst, dst_col_stride, coset_stride, src, src_stride, log_n, tab, tab_stride, kappa, st); break;
+        case 4: launch_head_R<4>(mode, k_on, g, dst, dst_col_stride, coset_stride, src, src_stride, log_n, tab, tab_stride, kappa, st); break;
         case 5: launch_head_R<5>(mode, k_on, g, dst, dst_col_stride, coset_stride, src, src_stride, log_n, tab, tab_stride, kappa, st); break;
         case 6: launch_head_R<6>(mode, k_on, g, dst, dst_col_stride, coset_stride, src, src_stride, log_n, tab, tab_stride, kappa, st); break;
         case 7: launch_head_R<7>(mode, k_on, g, dst, dst_col_stride, coset_stride, src, src_stride, log_n, tab, tab_stride, kappa, st); break;
