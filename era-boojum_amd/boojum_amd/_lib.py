@@ -23,6 +23,8 @@ SIGNATURES = {
     "bj_prepare": ([_u32], _int),
     "bj_precompute_twiddles_d": ([_u32, _int, _vp, _vp], _int),
     "bj_precompute_twiddles_h": ([_u32, _int, _u64p], _int),
+    "bj_precompute_twiddles_natural_d": ([_u32, _int, _vp, _vp], _int),
+    "bj_bitreverse_enumeration_d": ([_vp, _u32, _sz, _u32, _vp], _int),
     "bj_distribute_powers_d": ([_vp, _u32, _sz, _u32, _u64, _vp], _int),
     "bj_distribute_powers_h": ([_u64p, _sz, _u64], _int),
     "bj_fft_natural_to_bitreversed_d": ([_vp, _u32, _sz, _u32, _u64, _vp, _vp], _int),

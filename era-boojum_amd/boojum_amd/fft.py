@@ -65,6 +65,38 @@ def distribute_powers(cols, element):
     return cols
 
 
+def precompute_twiddles_for_fft_natural(fft_size, inverse=False, device=None):
+    """precompute_twiddles_for_fft_natural::<INVERSED> (utils.rs:127-155, fft/mod.rs:640-657):
+    omega^i (omega^-i), i < n/2, natural order.  int64 CUDA tensor of n/2 u64."""
+    import torch
+    log_n = _log2(fft_size)
+    if log_n == 0:
+        raise ValueError("twiddles need fft_size >= 2")
+    out = torch.empty(fft_size // 2, dtype=torch.int64, device=device or "cuda")
+    call("bj_precompute_twiddles_natural_d", log_n, 1 if inverse else 0, out.data_ptr(), stream_of(out))
+    return out
+
+
+def bitreverse_enumeration_inplace(cols):
+    """fft/mod.rs:41-155: bit-reversal permutation of each column, in place."""
+    v, c, n, stride = col_view(cols)
+    call("bj_bitreverse_enumeration_d", v.data_ptr(), c, stride, _log2(n), stream_of(v))
+    return cols
+
+
+# The reference's cache-friendly and MixedGL (SIMD-packed) variants compute the same transform
+# with another loop order or lane packing (fft/mod.rs:413-462, 493-623); on the GPU they are the
+# same batched kernels.
+fft_natural_to_bitreversed_cache_friendly = fft_natural_to_bitreversed
+fft_natural_to_bitreversed_mixedgl = fft_natural_to_bitreversed
+fft_natural_to_bitreversed_mixedgl_interleaving = fft_natural_to_bitreversed
+ifft_natural_to_natural_cache_friendly = ifft_natural_to_natural
+ifft_natural_to_natural_mixedgl = ifft_natural_to_natural
+ifft_natural_to_natural_mixedgl_interleaving = ifft_natural_to_natural
+precompute_twiddles_for_fft_wrapper = precompute_twiddles_for_fft
+precompute_twiddles_for_fft_natural_wrapper = precompute_twiddles_for_fft_natural
+
+
 # ------------------------------------------------------------------ host forms
 
 def _hp(a):

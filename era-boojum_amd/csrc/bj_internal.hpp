@@ -12,6 +12,8 @@ hipError_t launch_ntt_nb(uint64_t* dst, size_t dst_stride, const uint64_t* src, 
 hipError_t launch_bitrev_scale(uint64_t* dst, size_t dst_stride, const uint64_t* src, size_t src_stride,
                                uint32_t n_cols, uint32_t log_n, uint64_t scale, hipStream_t st);
 hipError_t launch_twiddles(uint64_t* out, uint32_t log_n, bool inverse, hipStream_t st);
+hipError_t launch_twiddles_natural(uint64_t* out, uint32_t log_n, bool inverse, hipStream_t st);
+hipError_t launch_bitrev_inplace(uint64_t* cols, size_t col_stride, uint32_t n_cols, uint32_t log_n, hipStream_t st);
 hipError_t launch_power_tables(uint64_t* lo, uint64_t* hi, uint32_t log_n, uint64_t e, uint64_t scale,
                                hipStream_t st);
 hipError_t launch_distribute(uint64_t* cols, size_t col_stride, uint32_t n_cols, uint32_t log_n,

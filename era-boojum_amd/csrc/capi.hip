@@ -352,6 +352,19 @@ int bj_precompute_twiddles_h(uint32_t log_n, int inverse, uint64_t* out_h) {
     return BJ_OK;
 }
 
+int bj_precompute_twiddles_natural_d(uint32_t log_n, int inverse, uint64_t* out_d, void* stream) {
+    if (int r = check_log_n(log_n)) return r;
+    if (log_n == 0) return fail(BJ_EINVAL, "twiddles need n >= 2");
+    HIP_TRY(bj::launch_twiddles_natural(out_d, log_n, inverse != 0, S(stream)), "twiddles");
+    return BJ_OK;
+}
+
+int bj_bitreverse_enumeration_d(uint64_t* cols, uint32_t n_cols, size_t col_stride, uint32_t log_n, void* stream) {
+    if (int r = check_log_n(log_n)) return r;
+    HIP_TRY(bj::launch_bitrev_inplace(cols, col_stride, n_cols, log_n, S(stream)), "bitreverse");
+    return BJ_OK;
+}
+
 int bj_distribute_powers_d(uint64_t* cols, uint32_t n_cols, size_t col_stride, uint32_t log_n, uint64_t element,
                            void* stream) {
     if (int r = check_log_n(log_n)) return r;

@@ -31,6 +31,30 @@ __global__ void twiddles_kernel(uint64_t* out, uint32_t log_n, uint64_t w) {
     }
 }
 
+// tw[i] = w^i, i < n/2: precompute_twiddles_for_fft_natural (utils.rs:127-155).
+__global__ void twiddles_natural_kernel(uint64_t* out, uint32_t log_n, uint64_t w) {
+    size_t half = (size_t)1 << (log_n - 1);
+    for (size_t i = blockIdx.x * (size_t)blockDim.x + threadIdx.x; i < half;
+         i += (size_t)gridDim.x * blockDim.x)
+        out[i] = gl::canon(gl::pow(w, i));
+}
+
+// In-place bit-reversal permutation of each column (bitreverse_enumeration_inplace,
+// fft/mod.rs:41-155): the pair (i, bitrev(i)), i < bitrev(i), is swapped by the thread of i;
+// values are moved, not re-represented.
+__global__ void bitrev_inplace_kernel(uint64_t* cols, size_t col_stride, uint32_t log_n) {
+    uint64_t* c = cols + (size_t)blockIdx.y * col_stride;
+    const size_t n = (size_t)1 << log_n;
+    for (size_t i = blockIdx.x * (size_t)blockDim.x + threadIdx.x; i < n; i += (size_t)gridDim.x * blockDim.x) {
+        const size_t r = log_n ? (size_t)gl::bitrev32((uint32_t)i, log_n) : 0;
+        if (i < r) {
+            const uint64_t a = c[i];
+            c[i] = c[r];
+            c[r] = a;
+        }
+    }
+}
+
 // Power tables for e^j = hi[j >> 12] * lo[j & 4095]: lo[t] = e^t (t < 4096),
 // hi[t] = e^(4096 t) (t < n_hi).  Optional factor `scale` folded into lo.
 __global__ void power_tables_kernel(uint64_t* lo, uint64_t* hi, uint32_t n_hi, uint64_t e, uint64_t scale) {
@@ -213,6 +237,27 @@ hipError_t launch_twiddles(uint64_t* out, uint32_t log_n, bool inverse, hipStrea
     size_t blocks = (half + 255) / 256;
     if (blocks > 4096) blocks = 4096;
     hipLaunchKernelGGL(twiddles_kernel, dim3((unsigned)blocks), dim3(256), 0, st, out, log_n, w);
+    return hipGetLastError();
+}
+
+hipError_t launch_twiddles_natural(uint64_t* out, uint32_t log_n, bool inverse, hipStream_t st) {
+    if (log_n == 0) return hipSuccess;
+    uint64_t w = gl::domain_generator(log_n);
+    if (inverse) w = gl::canon(gl::inv(w));
+    size_t half = (size_t)1 << (log_n - 1);
+    size_t blocks = (half + 255) / 256;
+    if (blocks > 4096) blocks = 4096;
+    hipLaunchKernelGGL(twiddles_natural_kernel, dim3((unsigned)blocks), dim3(256), 0, st, out, log_n, w);
+    return hipGetLastError();
+}
+
+hipError_t launch_bitrev_inplace(uint64_t* cols, size_t col_stride, uint32_t n_cols, uint32_t log_n, hipStream_t st) {
+    if (n_cols == 0 || log_n < 2) return hipSuccess;
+    size_t n = (size_t)1 << log_n;
+    size_t blocks = (n + 255) / 256;
+    if (blocks > 4096) blocks = 4096;
+    hipLaunchKernelGGL(bitrev_inplace_kernel, dim3((unsigned)blocks, n_cols), dim3(256), 0, st, cols, col_stride,
+                       log_n);
     return hipGetLastError();
 }
 

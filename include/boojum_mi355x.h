@@ -61,6 +61,15 @@ int bj_prepare(uint32_t log_n);
 int bj_precompute_twiddles_d(uint32_t log_n, int inverse, uint64_t* out_d, void* stream);
 int bj_precompute_twiddles_h(uint32_t log_n, int inverse, uint64_t* out_h);
 
+/* precompute_twiddles_for_fft_natural (cs/implementations/utils.rs:127-155, wrapper
+ * fft/mod.rs:640-657): w^i (or w^-i) for i < n/2 in natural order, canonical; out_d has n/2
+ * u64 on the device. */
+int bj_precompute_twiddles_natural_d(uint32_t log_n, int inverse, uint64_t* out_d, void* stream);
+
+/* bitreverse_enumeration_inplace (fft/mod.rs:41-155): the bit-reversal permutation of each of
+ * n_cols columns of n = 2^log_n, in place; values are moved unchanged. */
+int bj_bitreverse_enumeration_d(uint64_t* cols, uint32_t n_cols, size_t col_stride, uint32_t log_n, void* stream);
+
 /* distribute_powers (fft/mod.rs:308-317): col[j] *= element^j, for n_cols columns of
  * 2^log_n elements, column c at cols + c * col_stride. */
 int bj_distribute_powers_d(uint64_t* cols, uint32_t n_cols, size_t col_stride, uint32_t log_n,

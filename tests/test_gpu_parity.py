@@ -113,6 +113,22 @@ def test_ifft_natural_to_natural_batch(bj, log_n):
         eq(bj.field.to_host(t), want)
 
 
+@pytest.mark.parametrize("log_n", [1, 2, 5, 12, 20])
+def test_twiddles_natural_and_bitreverse(bj, log_n):
+    """precompute_twiddles_for_fft_natural = the bit-reversed table put back in natural order
+    (utils.rs:117-122 vs :127-155); bitreverse_enumeration_inplace is a pure permutation
+    (non-canonical values are moved unchanged)."""
+    n = 1 << log_n
+    for inv in (False, True):
+        nat = bj.field.to_host(bj.fft.precompute_twiddles_for_fft_natural(n, inv))
+        ref_br = O.precompute_twiddles(log_n, inv)
+        eq(nat, O.bitreverse(ref_br) if log_n > 1 else ref_br)
+    x = np.random.default_rng(log_n).integers(0, 2**64 - 1, size=(3, n), dtype=np.uint64, endpoint=True)
+    t = bj.field.to_device(x)
+    bj.fft.bitreverse_enumeration_inplace(t)
+    eq(bj.field.to_host(t), np.stack([O.bitreverse(r) for r in x]))
+
+
 def test_distribute_powers(bj):
     x = rand((2, 1 << 14), 5)
     t = bj.field.to_device(x)
