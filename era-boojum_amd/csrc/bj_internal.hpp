@@ -6,9 +6,6 @@
 
 namespace bj {
 
-hipError_t launch_ntt_nb(uint64_t* dst, size_t dst_stride, const uint64_t* src, size_t src_stride,
-                         uint32_t n_cols, uint32_t log_n, const uint64_t* tw, const uint64_t* pw_lo,
-                         const uint64_t* pw_hi, bool canon_out, hipStream_t st);
 hipError_t launch_bitrev_scale(uint64_t* dst, size_t dst_stride, const uint64_t* src, size_t src_stride,
                                uint32_t n_cols, uint32_t log_n, uint64_t scale, hipStream_t st);
 hipError_t launch_twiddles(uint64_t* out, uint32_t log_n, bool inverse, hipStream_t st);

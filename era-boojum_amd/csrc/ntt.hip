@@ -1,24 +1,13 @@
-// NTT kernels (gfx950): batched multi-column radix-2 Cooley-Tukey natural->bit-reversed
-// transforms, the iFFT bit-reverse/scale pass, coset power tables and twiddles.
-//
-// Algorithm = the reference's serial_ct_ntt_natural_to_bitreversed (fft/mod.rs:659-734):
-// stage s has 2^s groups; group k is the contiguous block [k*n/2^s, (k+1)*n/2^s) whose
-// butterflies pair j with j + n/2^(s+1) and multiply the upper input by tw[k], tw the
-// bit-reversed table of omega powers (utils.rs:88-125).  The stages are grouped into
-// passes; one pass runs R consecutive stages on LDS tiles.  After stage s0 the column
-// splits into 2^s0 independent blocks, and inside a block stages s0..s0+R-1 only couple
-// the 2^R elements {base + t*stride + o}, stride = n >> (s0+R).  A tile holds 2^R rows
-// (t) x W adjacent sub-problems (o), so every global access is a run of W contiguous
-// u64 (W*8 bytes) and every butterfly is done in LDS.  Same butterflies, same twiddles,
-// same order of operations per element as the reference => same field values.
+// NTT support kernels (gfx950): the iFFT bit-reverse/scale pass, the in-place bit reversal,
+// coset power tables, distribute_powers, twiddle tables (bit-reversed and natural order) and
+// the synthetic trace generator.  The transforms themselves are ntt_ct.hip (2^13..2^23) and
+// ntt_dif.hip (smaller sizes).
 #include <hip/hip_runtime.h>
 #include "gl.hpp"
 #include "bj_internal.hpp"
 
 namespace bj {
 
-constexpr int NTT_THREADS = 256;
-constexpr int TILE_LOG = 12;  // 4096 u64 = 32 KiB of LDS per block
 
 // --------------------------------------------------------------- twiddles
 // tw[i] = w^bitrev_{log_n - 1}(i), i < n/2 (utils.rs:117-122: powers, then bitreverse).
@@ -61,64 +50,6 @@ __global__ void power_tables_kernel(uint64_t* lo, uint64_t* hi, uint32_t n_hi, u
     uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
     if (i < 4096) lo[i] = gl::canon(gl::mul(gl::pow(e, i), scale));
     if (i < n_hi) hi[i] = gl::canon(gl::pow(e, (uint64_t)i * 4096));
-}
-
-// ----------------------------------------------------------------- NTT pass
-// Grid: x = tiles per column, y = columns.  src may alias dst (in place).
-// pw_lo/pw_hi (nullable): multiply element j by pw_hi[j>>12]*pw_lo[j&4095] on load
-// (distribute_powers, fused into the first pass).
-__global__ __launch_bounds__(NTT_THREADS) void ntt_pass_kernel(
-    uint64_t* dst, size_t dst_stride, const uint64_t* src, size_t src_stride, uint32_t log_n,
-    uint32_t s0, uint32_t R, uint32_t logW, const uint64_t* __restrict__ tw,
-    const uint64_t* __restrict__ pw_lo, const uint64_t* __restrict__ pw_hi, int canon_out) {
-    __shared__ uint64_t tile[1 << TILE_LOG];
-    const uint32_t tid = threadIdx.x;
-    const size_t col = blockIdx.y;
-    const uint32_t tile_log = R + logW;
-    const uint32_t tile_n = 1u << tile_log;
-    const uint32_t W = 1u << logW;
-    const size_t n = (size_t)1 << log_n;
-    const size_t stride = n >> (s0 + R);
-    const size_t oblocks = stride >> logW;
-    const size_t q = blockIdx.x;
-    const size_t b = q / oblocks;
-    const size_t ob = q - b * oblocks;
-    const size_t base = b * (n >> s0) + (ob << logW);
-    const uint64_t* s = src + col * src_stride;
-    uint64_t* d = dst + col * dst_stride;
-
-    for (uint32_t e = tid; e < tile_n; e += NTT_THREADS) {
-        const uint32_t t = e >> logW, w = e & (W - 1);
-        const size_t j = base + (size_t)t * stride + w;
-        uint64_t v = s[j];
-        if (pw_lo) v = gl::mul(v, gl::mul(pw_hi[j >> 12], pw_lo[j & 4095]));
-        tile[e] = v;
-    }
-    __syncthreads();
-    for (uint32_t u = 0; u < R; u++) {
-        const uint32_t lh = R - 1 - u;  // log2(half) in rows
-        const uint32_t half = 1u << lh;
-        for (uint32_t p = tid; p < tile_n / 2; p += NTT_THREADS) {
-            const uint32_t w = p & (W - 1);
-            const uint32_t pp = p >> logW;
-            const uint32_t g = pp >> lh;
-            const uint32_t within = pp & (half - 1);
-            const uint32_t t1 = (g << (lh + 1)) + within;
-            const uint32_t i1 = (t1 << logW) + w;
-            const uint32_t i2 = i1 + (half << logW);
-            const uint64_t x = tile[i1];
-            const uint64_t y = gl::mul(tile[i2], tw[(b << u) + g]);
-            tile[i1] = gl::add(x, y);
-            tile[i2] = gl::sub(x, y);
-        }
-        __syncthreads();
-    }
-    for (uint32_t e = tid; e < tile_n; e += NTT_THREADS) {
-        const uint32_t t = e >> logW, w = e & (W - 1);
-        const size_t j = base + (size_t)t * stride + w;
-        uint64_t v = tile[e];
-        d[j] = canon_out ? gl::canon(v) : v;
-    }
 }
 
 // ------------------------------------------------------- bit-reverse + scale
@@ -175,44 +106,6 @@ static inline dim3 grid2(size_t x, uint32_t y) { return dim3((unsigned)x, y, 1);
 
 // Full natural->bit-reversed transform of n_cols columns (src -> dst; src may == dst),
 // with optional coset power tables applied on load.
-hipError_t launch_ntt_nb(uint64_t* dst, size_t dst_stride, const uint64_t* src, size_t src_stride,
-                         uint32_t n_cols, uint32_t log_n, const uint64_t* tw, const uint64_t* pw_lo,
-                         const uint64_t* pw_hi, bool canon_out, hipStream_t st) {
-    if (n_cols == 0) return hipSuccess;
-    if (log_n == 0) {
-        // n == 1: transform is the identity (fft/mod.rs:666-668); coset power is e^0 = 1.
-        hipLaunchKernelGGL(scale_copy_kernel, grid2(1, n_cols), dim3(64), 0, st, dst, dst_stride, src, src_stride,
-                           (size_t)1, (uint64_t)1);
-        return hipGetLastError();
-    }
-    // Plan: a last pass of min(log_n, 12) stages on contiguous tiles; the stages before it
-    // split into passes of <= 8 stages (W = 2^(12-R) adjacent sub-problems per tile).
-    const uint32_t last = log_n < (uint32_t)TILE_LOG ? log_n : (uint32_t)TILE_LOG;
-    const uint32_t front = log_n - last;
-    const uint32_t npass_front = (front + 7) / 8;
-    uint32_t s0 = 0;
-    const uint64_t* cur_src = src;
-    size_t cur_stride = src_stride;
-    for (uint32_t p = 0; p < npass_front; p++) {
-        const uint32_t R = (front - s0 + (npass_front - p) - 1) / (npass_front - p);
-        const uint32_t logW = TILE_LOG - R;
-        const size_t tiles = ((size_t)1 << log_n) >> TILE_LOG;
-        hipLaunchKernelGGL(ntt_pass_kernel, grid2(tiles, n_cols), dim3(NTT_THREADS), 0, st, dst, dst_stride,
-                           cur_src, cur_stride, log_n, s0, R, logW, tw, p == 0 ? pw_lo : nullptr,
-                           p == 0 ? pw_hi : nullptr, 0);
-        s0 += R;
-        cur_src = dst;
-        cur_stride = dst_stride;
-    }
-    {
-        const size_t tiles = ((size_t)1 << log_n) >> last;
-        hipLaunchKernelGGL(ntt_pass_kernel, grid2(tiles, n_cols), dim3(NTT_THREADS), 0, st, dst, dst_stride,
-                           cur_src, cur_stride, log_n, s0, last, 0u, tw, npass_front == 0 ? pw_lo : nullptr,
-                           npass_front == 0 ? pw_hi : nullptr, canon_out ? 1 : 0);
-    }
-    return hipGetLastError();
-}
-
 hipError_t launch_bitrev_scale(uint64_t* dst, size_t dst_stride, const uint64_t* src, size_t src_stride,
                                uint32_t n_cols, uint32_t log_n, uint64_t scale, hipStream_t st) {
     if (n_cols == 0) return hipSuccess;
