@@ -74,8 +74,20 @@ def _log2(n):
     return n.bit_length() - 1
 
 
+# tree hashers whose leaf message can be continued over column ranges (the column pipeline)
+PARTIAL_HASHERS = ("poseidon2", "blake2s")
+
+
 class HipShardOps:
-    """The product compute steps, through libboojum_mi355x.so on the current stream."""
+    """The product compute steps, through libboojum_mi355x.so on the current stream.
+    hasher: the MerkleTreeWithCap tree hasher (boojum_amd.merkle.HASHERS)."""
+
+    def __init__(self, hasher="poseidon2"):
+        from .merkle import HASHERS
+        if hasher not in HASHERS:
+            raise ValueError("unknown tree hasher %r" % (hasher,))
+        self.hasher = hasher
+        self._leaves_fn, self._nodes_fn = HASHERS[hasher][1], HASHERS[hasher][3]
 
     def coeffs(self, trace, out, log_n):
         call("bj_lde_coeffs_d", trace.data_ptr(), trace.shape[0], trace.stride(0), log_n, out.data_ptr(),
@@ -94,13 +106,23 @@ class HipShardOps:
         call("bj_lde_shard_d", coeffs.data_ptr(), coeffs.shape[0], coeffs.stride(0), log_n, log_lde, log_shards,
              shard, None if work is None else work.data_ptr(), lde.data_ptr(), stream_of(lde))
 
-    def leaves(self, lde, out, cap_in=None, final=True):
+    def leaves(self, lde, out, cap_in=None, final=True, cols_before=0):
+        """Leaf messages over the column range lde (C_k, m), continuing from cap_in (the carried
+        sponge capacity / Blake2s chaining value after cols_before columns) when given."""
         c, m = lde.shape
-        call("bj_merkle_leaves_partial_d", lde.data_ptr(), c, lde.stride(0), m,
-             None if cap_in is None else cap_in.data_ptr(), out.data_ptr(), 1 if final else 0, stream_of(out))
+        if self.hasher == "poseidon2":
+            call("bj_merkle_leaves_partial_d", lde.data_ptr(), c, lde.stride(0), m,
+                 None if cap_in is None else cap_in.data_ptr(), out.data_ptr(), 1 if final else 0, stream_of(out))
+        elif self.hasher == "blake2s":
+            call("bj_blake2s_leaves_partial_d", lde.data_ptr(), c, lde.stride(0), m, cols_before,
+                 None if cap_in is None else cap_in.data_ptr(), out.data_ptr(), 1 if final else 0, stream_of(out))
+        else:
+            if cap_in is not None or not final:
+                raise ValueError("%s leaves cannot be continued over column ranges" % self.hasher)
+            call(self._leaves_fn, lde.data_ptr(), c, lde.stride(0), m, out.data_ptr(), stream_of(out))
 
     def nodes(self, leaves, cap_size, out):
-        call("bj_merkle_nodes_d", leaves.data_ptr(), leaves.shape[0], cap_size, out.data_ptr(), stream_of(out))
+        call(self._nodes_fn, leaves.data_ptr(), leaves.shape[0], cap_size, out.data_ptr(), stream_of(out))
 
     def synthetic(self, out, log_n, first_col):
         call("bj_fill_synthetic_d", out.data_ptr(), out.shape[0], out.stride(0), log_n, 42, first_col,
@@ -166,7 +188,7 @@ class ShardedWorkspace:
     """
 
     def __init__(self, n_cols, log_n, log_lde, cap_size, rank, world, device="cuda", group=None, ops=None,
-                 max_chunk_cols=MAX_CHUNK_COLS, fold_exchange=True):
+                 max_chunk_cols=MAX_CHUNK_COLS, fold_exchange=True, hasher="poseidon2"):
         log_g = _log2(world)
         _log2(cap_size)
         if n_cols % world:
@@ -179,7 +201,8 @@ class ShardedWorkspace:
             raise ValueError("tree size must exceed cap size")
         self.n_cols, self.log_n, self.log_lde, self.cap_size = n_cols, log_n, log_lde, cap_size
         self.rank, self.world, self.log_g, self.group = rank, world, log_g, group
-        self.ops = ops if ops is not None else HipShardOps()
+        self.ops = ops if ops is not None else HipShardOps(hasher)
+        self.hasher = getattr(self.ops, "hasher", hasher)
         n = 1 << log_n
         self.m = m = (n << log_lde) >> log_g
         self.cols_per_rank = n_cols // world
@@ -188,7 +211,7 @@ class ShardedWorkspace:
             raise ValueError("each shard needs more leaves than its cap slice")
         # column pipeline geometry
         unit = _chunk_unit(world)
-        self.pipelined = self.cols_per_rank % unit == 0
+        self.pipelined = self.cols_per_rank % unit == 0 and self.hasher in PARTIAL_HASHERS
         if self.pipelined:
             self.schedule = _chunk_schedule(self.cols_per_rank, unit, max_chunk_cols)
         else:
@@ -306,7 +329,8 @@ def sharded_witness_commit(trace_shard, ws, timer=None):
         timer.stop("lde")
         last = k == ws.n_chunks - 1
         timer.start("leaves")
-        ops.leaves(ws.lde[cols], ws.leaves if last else ws.state, cap_in=None if k == 0 else ws.state, final=last)
+        ops.leaves(ws.lde[cols], ws.leaves if last else ws.state, cap_in=None if k == 0 else ws.state, final=last,
+                   cols_before=c0)
         timer.stop("leaves")
     timer.start("nodes")
     ops.nodes(ws.leaves, ws.cap_local, ws.nodes)

@@ -458,6 +458,41 @@ static void b2s_leaf_strided(const u64* elems, size_t count, size_t stride, u64*
 
 void bjo_blake2s_leaf(const u64* elems, size_t count, u64* out4) { b2s_leaf_strided(elems, count, 1, out4); }
 
+/* One leaf's message continued over a column range (the multi-GPU column pipeline):
+ * h_in = the chaining value after `before` elements (a multiple of 8; NULL when 0).  With
+ * final == 0 (count a multiple of 8) every block is compressed as more data follows and
+ * out4 = the new chaining value; with final != 0 the last block carries the final flag and
+ * out4 = the digest.  Chaining ranges gives exactly bjo_blake2s_leaf of the whole message. */
+void bjo_blake2s_leaf_partial(const u64* h_in, const u64* elems, size_t count, uint64_t before, int final_,
+                              u64* out4) {
+    uint32_t h[8], m[16];
+    if (h_in) {
+        for (int i = 0; i < 4; i++) { h[2 * i] = (uint32_t)h_in[i]; h[2 * i + 1] = (uint32_t)(h_in[i] >> 32); }
+    } else {
+        for (int i = 0; i < 8; i++) h[i] = B2S_IV[i];
+        h[0] ^= 0x01010000u ^ 32u;
+    }
+    uint64_t bytes = 8 * before;
+    size_t k = 0;
+    size_t nonfinal = final_ ? (count ? (count - 1) / 8 : 0) : count / 8;
+    for (size_t g = 0; g < nonfinal; g++, k += 8) {
+        for (int i = 0; i < 8; i++) { u64 v = gl_canon(elems[k + i]); m[2 * i] = (uint32_t)v; m[2 * i + 1] = (uint32_t)(v >> 32); }
+        bytes += 64;
+        b2s_compress(h, m, bytes, 0);
+    }
+    if (final_) {
+        size_t rem = count - k;
+        for (int i = 0; i < 8; i++) {
+            u64 v = (size_t)i < rem ? gl_canon(elems[k + i]) : 0;
+            m[2 * i] = (uint32_t)v;
+            m[2 * i + 1] = (uint32_t)(v >> 32);
+        }
+        bytes += 8 * rem;
+        b2s_compress(h, m, bytes, 1);
+    }
+    for (int i = 0; i < 4; i++) out4[i] = ((u64)h[2 * i + 1] << 32) | h[2 * i];
+}
+
 void bjo_blake2s_node(const u64* l, const u64* r, u64* out4) {
     uint8_t buf[64];
     memcpy(buf, l, 32);

@@ -54,6 +54,7 @@ def lib():
         L.bjo_blake2s.argtypes = [ctypes.c_char_p, sz, ctypes.c_char_p]
         L.bjo_blake2s_leaf.argtypes = [_u64p, sz, _u64p]
         L.bjo_blake2s_node.argtypes = [_u64p, _u64p, _u64p]
+        L.bjo_blake2s_leaf_partial.argtypes = [_u64p, _u64p, sz, u64, i, _u64p]
         L.bjo_keccak256.argtypes = [ctypes.c_char_p, sz, ctypes.c_char_p, i]
         L.bjo_keccak_leaf.argtypes = [_u64p, sz, _u64p]
         L.bjo_keccak_node.argtypes = [_u64p, _u64p, _u64p]
@@ -198,6 +199,18 @@ def blake2s_leaf(elems):
         e = np.zeros(1, np.uint64)
     out = np.zeros(4, dtype=np.uint64)
     lib().bjo_blake2s_leaf(_p(e), n, _p(out))
+    return out
+
+
+def blake2s_leaf_partial(h_in, elems, before, final):
+    """One leaf's Blake2s message continued over a column range (bjo_blake2s_leaf_partial)."""
+    e = _u64(elems)
+    n = e.size
+    if n == 0:
+        e = np.zeros(1, np.uint64)
+    out = np.zeros(4, dtype=np.uint64)
+    hp = None if h_in is None else _p(_u64(h_in))
+    lib().bjo_blake2s_leaf_partial(hp, _p(e), n, before, 1 if final else 0, _p(out))
     return out
 
 

@@ -15,6 +15,9 @@ def _np(t):
 
 
 class CpuShardOps:
+    def __init__(self, hasher="poseidon2"):
+        self.hasher = hasher
+
     def prepare(self, log_n):
         pass
 
@@ -64,8 +67,18 @@ class CpuShardOps:
             flat = np.concatenate([O.fft_natural_to_bitreversed(mono, int(s)) for s in cosets])
             _np(lde)[c] = flat[shard * m:(shard + 1) * m]
 
-    def leaves(self, lde, out, cap_in=None, final=True):
+    def leaves(self, lde, out, cap_in=None, final=True, cols_before=0):
         src = _np(lde)
+        if self.hasher == "blake2s":
+            cin = None if cap_in is None else _np(cap_in).copy()
+            _np(out)[:] = np.stack([O.blake2s_leaf_partial(None if cin is None else cin[r],
+                                                           np.ascontiguousarray(src[:, r]), cols_before, final)
+                                    for r in range(src.shape[1])])
+            return
+        if self.hasher == "keccak256":
+            assert cap_in is None and final
+            _np(out)[:] = np.stack([O.keccak_leaf(np.ascontiguousarray(src[:, r])) for r in range(src.shape[1])])
+            return
         if cap_in is None and final:
             _np(out)[:] = np.stack([O.hash_into_leaf(np.ascontiguousarray(src[:, r])) for r in range(src.shape[1])])
             return
@@ -91,10 +104,11 @@ class CpuShardOps:
     def nodes(self, leaves, cap_size, out):
         lv = _np(leaves)
         # merkle_construct hashes leaves from elements; rebuild the node levels directly
+        node = {"poseidon2": O.hash_into_node, "blake2s": O.blake2s_node, "keccak256": O.keccak_node}[self.hasher]
         cur = lv.copy()
         res = []
         while cur.shape[0] > cap_size:
-            nxt = np.stack([O.hash_into_node(cur[2 * i], cur[2 * i + 1]) for i in range(cur.shape[0] // 2)])
+            nxt = np.stack([node(cur[2 * i], cur[2 * i + 1]) for i in range(cur.shape[0] // 2)])
             res.append(nxt)
             cur = nxt
         _np(out)[:] = np.concatenate(res)

@@ -20,14 +20,16 @@ def run(rank, world, port, cfg, outdir, device, paths):
         from boojum_amd.sharded import ShardedWorkspace, sharded_witness_commit
         n_cols, log_n, log_lde, cap = cfg[:4]
         extra = {"max_chunk_cols": 8 * cfg[4]} if len(cfg) > 4 and cfg[4] else {}
-        if len(cfg) > 5:
+        if len(cfg) > 5 and cfg[5] is not None:
             extra["fold_exchange"] = cfg[5]
+        hasher = cfg[6] if len(cfg) > 6 else "poseidon2"
         if device == "cpu":
             from shard_cpu_ops import CpuShardOps
-            ops, dev = CpuShardOps(), "cpu"
+            ops, dev = CpuShardOps(hasher), "cpu"
         else:
             torch.cuda.set_device(0)
             ops, dev = None, "cuda:0"
+            extra["hasher"] = hasher
         ws = ShardedWorkspace(n_cols, log_n, log_lde, cap, rank, world, device=dev, ops=ops, **extra)
         tr = ws.synthetic_trace_shard()
         sharded_witness_commit(tr, ws)

@@ -26,7 +26,13 @@ def run_and_check(world, cfg, tmp_path, device):
     n_cols, log_n, log_lde, cap = cfg[:4]
     n, nl = 1 << log_n, 1 << (log_n + log_lde)
     m = nl // world
-    ref = O.lde_commit(O.synthetic_trace(n_cols, log_n), log_lde, cap, threads=4)
+    hasher = cfg[6] if len(cfg) > 6 else "poseidon2"
+    if hasher == "poseidon2":
+        ref = O.lde_commit(O.synthetic_trace(n_cols, log_n), log_lde, cap, threads=4)
+    else:
+        _, lde = O.lde(O.synthetic_trace(n_cols, log_n), log_lde, threads=4)
+        leaves, nodes, _, cap_ref = O.merkle_construct(lde.reshape(n_cols, nl), cap, threads=4, hasher=hasher)
+        ref = {"lde": lde, "leaves": leaves, "nodes": nodes, "cap": cap_ref}
     lde_flat = ref["lde"].reshape(n_cols, nl)
     # global node levels: level k (k >= 1) holds nl >> k digests
     offs, o = [], 0
@@ -57,4 +63,4 @@ def run_and_check(world, cfg, tmp_path, device):
             assert np.array_equal(r["q_elems"][j], lde_flat[:, idx]), "rank %d query %d elements" % (P, idx)
             assert np.array_equal(r["q_leaf"][j], leaf), "rank %d query %d leaf" % (P, idx)
             assert np.array_equal(r["q_path"][j], path), "rank %d query %d path" % (P, idx)
-            assert O.verify_proof_over_cap(r["q_path"][j], ref["cap"], r["q_leaf"][j], idx)
+            assert O.verify_proof_over_cap(r["q_path"][j], ref["cap"], r["q_leaf"][j], idx, hasher=hasher)

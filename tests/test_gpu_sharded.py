@@ -90,7 +90,8 @@ def test_lde_shard_errors(torch_mod):
 
 @pytest.mark.parametrize("world,cfg", [(2, (8, 10, 1, 16)), (4, (8, 9, 1, 2)), (2, (48, 10, 2, 16, 1)),
                                        (4, (64, 12, 1, 4, 1)), (8, (64, 9, 1, 16)), (2, (256, 9, 1, 16)),
-                                       (4, (64, 12, 1, 4, 1, False)), (8, (128, 14, 2, 16))])
+                                       (4, (64, 12, 1, 4, 1, False)), (8, (128, 14, 2, 16)),
+                                       (4, (64, 12, 1, 4, 1, None, "blake2s")), (2, (32, 10, 1, 16, 0, None, "keccak256"))])
 def test_sharded_commit_multirank_one_gpu(torch_mod, world, cfg, tmp_path):
     from sharded_check import run_and_check
     run_and_check(world, cfg, tmp_path, "cuda")

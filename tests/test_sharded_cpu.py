@@ -24,6 +24,9 @@ from sharded_check import run_and_check
     (4, (4, 4, 1, 2, 0, False)),      # G > D through the all-gather of unfolded coefficients
     (4, (64, 4, 1, 2, 1, False)),     # the same, column-pipelined
     (8, (8, 4, 1, 16)),               # G = 4 D: fold by 4 on the sender, all-to-all
+    (2, (48, 4, 2, 8, 1, None, "blake2s")),    # Blake2s tree, pipelined: chaining value carried
+    (4, (8, 4, 1, 2, 0, None, "blake2s")),     # Blake2s tree, G > D, cap < G
+    (2, (32, 4, 1, 4, 1, None, "keccak256")),  # Keccak256 tree: one chunk (no continuation)
 ])
 def test_sharded_commit_gloo(world, cfg, tmp_path):
     run_and_check(world, cfg, tmp_path, "cpu")
