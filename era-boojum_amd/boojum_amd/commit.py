@@ -71,6 +71,31 @@ def witness_commit(trace, lde_degree, cap_size, workspace=None, hasher="poseidon
     return ws
 
 
+class CommitGraph:
+    """The whole commit of a fixed trace buffer, captured once as a HIP graph and replayed.
+
+    A prover that commits many traces of one shape (or the bench) refills `trace` in place and
+    calls replay(): one graph launch instead of the commit's ~10-30 kernel launches, which is
+    what bounds the small shapes (C1, C5). The first commit runs eagerly, outside the capture,
+    so every twiddle / power table the kernels read is created (and cached) before capturing;
+    the captured calls then only launch kernels on the capture stream."""
+
+    def __init__(self, trace, lde_degree, cap_size, hasher="poseidon2", workspace=None):
+        self.trace = trace
+        self.args = (lde_degree, cap_size)
+        self.hasher = hasher
+        self.ws = witness_commit(trace, lde_degree, cap_size, workspace, hasher)
+        torch.cuda.synchronize()
+        self.graph = torch.cuda.CUDAGraph()
+        with torch.cuda.graph(self.graph):
+            witness_commit(trace, lde_degree, cap_size, self.ws, hasher)
+
+    def replay(self):
+        """Commit the current contents of `trace` (asynchronous on the current stream)."""
+        self.graph.replay()
+        return self.ws
+
+
 def synthetic_trace(n_cols, log_n, seed=42, first_col=0, device="cuda", out=None):
     """Device-generated synthetic trace: splitmix64(seed + c*n + r) mod p."""
     n = 1 << log_n

@@ -91,6 +91,25 @@ def test_c5_sha256_shape_witness_commit(bj):
     eq(bj.field.to_host(ws.leaves), ref["leaves"], "leaves")
 
 
+@pytest.mark.parametrize("hasher", ["poseidon2", "blake2s"])
+def test_commit_graph_replay(bj, hasher):
+    """commit.CommitGraph: the commit captured once as a HIP graph; refilling the trace buffer in
+    place and replaying commits the new contents (not a cached result)."""
+    torch = bj.torch
+    c, log_n, log_d, cap = 24, 14, 2, 16
+    tr = bj.commit.synthetic_trace(c, log_n)
+    g = bj.commit.CommitGraph(tr, 1 << log_d, cap, hasher=hasher)
+    for seed in (42, 7):
+        bj.commit.synthetic_trace(c, log_n, seed=seed, out=tr)
+        ws = g.replay()
+        torch.cuda.synchronize()
+        x = O.synthetic_trace(c, log_n, seed=seed)
+        _, l_ref = O.lde(x, log_d, threads=THREADS)
+        leaves, _, _, cap_ref = O.merkle_construct(l_ref.reshape(c, -1), cap, threads=THREADS, hasher=hasher)
+        eq(bj.field.to_host(ws.leaves), leaves, "graph leaves seed %d" % seed)
+        eq(bj.field.to_host(ws.cap), cap_ref, "graph cap seed %d" % seed)
+
+
 def test_memcopy_serialization_roundtrip(bj):
     """A GPU tree and LDE written in the reference's MemcopySerializable layout read back equal."""
     import io
