@@ -91,7 +91,7 @@ def test_twiddles(bj, log_n):
         eq(bj.field.to_host(t), O.precompute_twiddles(log_n, inv))
 
 
-@pytest.mark.parametrize("log_n", [0, 1, 2, 4, 7, 11, 12, 13, 15, 17, 18, 20, 21, 23])
+@pytest.mark.parametrize("log_n", [0, 1, 2, 4, 7, 11, 12, 13, 14, 15, 16, 17, 18, 20, 21, 23])
 def test_fft_natural_to_bitreversed_batch(bj, log_n):
     c = 3 if log_n < 18 else 1
     x = rand((c, 1 << log_n), log_n)
@@ -103,7 +103,7 @@ def test_fft_natural_to_bitreversed_batch(bj, log_n):
         eq(bj.field.to_host(t), want)
 
 
-@pytest.mark.parametrize("log_n", [0, 1, 2, 3, 6, 10, 12, 13, 14, 18, 19, 22, 23])
+@pytest.mark.parametrize("log_n", [0, 1, 2, 3, 6, 10, 12, 13, 14, 15, 16, 17, 18, 19, 22, 23])
 def test_ifft_natural_to_natural_batch(bj, log_n):
     x = rand((2, 1 << log_n), 50 + log_n)
     for coset in (1, 7):
@@ -180,6 +180,7 @@ def test_host_seams_concurrent_threads(bj):
 # -------------------------------------------------------------------- LDE
 
 @pytest.mark.parametrize("c,log_n,log_d", [(1, 0, 1), (2, 1, 1), (3, 3, 2), (5, 6, 3), (4, 12, 1), (3, 13, 2),
+                                           (3, 14, 3), (5, 15, 1), (1, 16, 2), (7, 13, 3),
                                            (2, 16, 3), (1, 17, 1), (2, 18, 2), (1, 19, 3), (1, 20, 1)])
 def test_lde_batch(bj, c, log_n, log_d):
     x = rand((c, 1 << log_n), c * 100 + log_n)
