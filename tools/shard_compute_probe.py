@@ -45,6 +45,33 @@ def main():
                        final=last)
         ops.nodes(ws.leaves, ws.cap_local, ws.nodes)
 
+    class TimedOps:
+        """Wraps the ops object: events around every call, summed per op name."""
+
+        def __init__(self, inner):
+            self.inner, self.ev = inner, []
+
+        def __getattr__(self, name):
+            fn = getattr(self.inner, name)
+            if not callable(fn):
+                return fn
+
+            def run(*a, **k):
+                s, e = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+                s.record()
+                r = fn(*a, **k)
+                e.record()
+                self.ev.append((name, s, e))
+                return r
+            return run
+
+        def totals(self, reps):
+            torch.cuda.synchronize()
+            acc = {}
+            for name, s, e in self.ev:
+                acc[name] = acc.get(name, 0.0) + s.elapsed_time(e)
+            return {k: round(v / reps, 3) for k, v in acc.items()}
+
     runs = [(w, True) for w in (1, 2, 4, 8)] + [(w, False) for w in (8,) if w > (1 << log_lde)]
     for world, fold in runs:
         ws = sharded.ShardedWorkspace(n_cols, log_n, log_lde, cap, 0, world, device="cuda", fold_exchange=fold)
@@ -58,8 +85,14 @@ def main():
         e.record()
         torch.cuda.synchronize()
         ms = s.elapsed_time(e) / 3
-        out["%d%s" % (world, "" if fold or world <= (1 << log_lde) else "_allgather")] = {"ms_per_rank": round(ms, 2), "chunks": ws.n_chunks,
-                      "ideal_elems_per_s": n_cols * (1 << log_n) / (ms * 1e-3)}
+        timed = TimedOps(ws.ops)
+        ws.ops = timed
+        compute(ws, tr)
+        phases = timed.totals(1)
+        ws.ops = timed.inner
+        out["%d%s" % (world, "" if fold or world <= (1 << log_lde) else "_allgather")] = {
+            "ms_per_rank": round(ms, 2), "chunks": ws.n_chunks,
+            "ideal_elems_per_s": n_cols * (1 << log_n) / (ms * 1e-3), "phase_ms": phases}
         del ws, tr
         torch.cuda.empty_cache()
     print(json.dumps({"config": cfg, "per_rank_compute": out}))
