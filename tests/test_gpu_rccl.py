@@ -3,7 +3,6 @@ the box: the in-place all-gather and the all-to-all of boojum_amd/sharded.py wit
 ordering the compute stream, under the bench's process-group options (high-priority stream).
 A one-rank group cannot show bandwidth or overlap; it checks that the calls, options and
 stream ordering the 8-GPU run depends on are accepted by this torch/RCCL build."""
-import os
 
 import pytest
 
