@@ -97,6 +97,9 @@ __device__ __forceinline__ uint64_t canon_u64(uint64_t v) {
 
 // ------------------------------------------------------------------- head
 
+// Padded LDS layout shared by the head exchange and the tail: element e at slot e + (e >> 5).
+constexpr int PAD_LDS = TILE + TILE / 32;
+
 template <int LOGW>
 __device__ __forceinline__ uint32_t swz_head(uint32_t e) {
     constexpr uint32_t m = LOGW >= 5 ? 0u : ((32u >> LOGW) - 1u);
@@ -169,7 +172,7 @@ __global__ __launch_bounds__(NT, 2) void ct_head_kernel(uint64_t* dst, size_t ds
     constexpr int LOGW = 13 - R;
     constexpr uint32_t W = 1u << LOGW;
     constexpr uint32_t T = 1u << (R - 5);
-    __shared__ uint64_t lds[TILE];
+    __shared__ uint64_t lds[PAD_LDS];
     const uint32_t tid = threadIdx.x;
     const size_t n = (size_t)1 << log_n;
     const size_t S = n >> R;
@@ -216,11 +219,16 @@ __global__ __launch_bounds__(NT, 2) void ct_head_kernel(uint64_t* dst, size_t ds
         ct_stage<1>(x, wa);
     }
     if constexpr (MODE == 1) __syncthreads();  // gather reads of lds done
+    // phase A' -> B' exchange in the padded layout: writes e = tid + 256 k at
+    // (tid + (tid >> 5)) + 264 k, reads e = (32 s + k) W + w at 33 W s + w + (w >> 5) + kW + (kW >> 5):
+    // per-thread bases, compile-time offsets, conflict free for every R
+    const uint32_t pa = tid + (tid >> 5);
+    const uint32_t pd = 33 * W * s + w + (w >> 5);
 #pragma unroll
-    for (int k = 0; k < PT; k++) lds[swz_head<LOGW>((s + T * k) * W + w)] = x[k];
+    for (int k = 0; k < PT; k++) lds[pa + 264 * k] = x[k];
     __syncthreads();
 #pragma unroll
-    for (int k = 0; k < PT; k++) x[k] = lds[swz_head<LOGW>((32 * s + k) * W + w)];
+    for (int k = 0; k < PT; k++) x[k] = lds[pd + k * W + ((k * W) >> 5)];
     head_b_stage<R, 5>(x, ct, s);
     uint64_t* dc = dst + (size_t)col * dst_col_stride + (size_t)coset * coset_stride;
 #pragma unroll
@@ -309,7 +317,20 @@ __global__ __launch_bounds__(NT, 2) void ct_head_small_kernel(uint64_t* dst, siz
 
 // ------------------------------------------------------------------- tail
 
-__device__ __forceinline__ uint32_t swz_tail(uint32_t e) { return e ^ ((e >> 5) & 31); }
+// Tail LDS layout: element e at slot e + (e >> 5) (one pad word per 32). For the three
+// exchange patterns the slot splits into a per-thread base plus a compile-time offset per
+// register k, so every ds_read / ds_write takes its k-part as an immediate offset and needs no
+// address VALU:
+//   A: e = t + 256 k                         -> (t + (t >> 5)) + 264 k
+//   B: e = (thi << 8) | (k << 3) | tlo       -> (264 thi + tlo) + 8 k + (k >> 2)
+//   C: e = 32 t + k                          -> 33 t + k
+// and each is bank-conflict free for ds_read_b64 / ds_write_b64 (32 consecutive lanes hit 32
+// distinct 8-byte slots mod 32, up to one pad skip in pattern A).
+__device__ __forceinline__ uint32_t tail_base_a(uint32_t t) { return t + (t >> 5); }
+__device__ __forceinline__ uint32_t tail_base_b(uint32_t thi, uint32_t tlo) { return 264 * thi + tlo; }
+__device__ __forceinline__ uint32_t tail_base_c(uint32_t t) { return 33 * t; }
+__device__ __forceinline__ constexpr uint32_t tail_off_a(int k) { return 264 * k; }
+__device__ __forceinline__ constexpr uint32_t tail_off_b(int k) { return 8 * k + (k >> 2); }
 
 // phase A (element t + 256 k, local stage v = 0..4): group (q << v) + (lo(q) >> (5 - v)),
 // wave-uniform.
@@ -344,7 +365,7 @@ __device__ __forceinline__ void tw_ct_tailC(uint64_t* w, const uint64_t* __restr
 __global__ __launch_bounds__(NT, 2) void ct_tail_kernel(uint64_t* dst, size_t dst_col_stride, size_t coset_stride,
                                                         uint32_t log_n, const uint64_t* __restrict__ tab,
                                                         size_t tab_stride, int canon_out) {
-    __shared__ uint64_t lds[TILE];
+    __shared__ uint64_t lds[PAD_LDS];
     const uint32_t t = threadIdx.x;
     const size_t q = blockIdx.y;
     const uint32_t u0 = log_n - 13;
@@ -363,13 +384,14 @@ __global__ __launch_bounds__(NT, 2) void ct_tail_kernel(uint64_t* dst, size_t ds
     tw_ct_tailA<4>(wa, ct, u0, q);
     ct_stage<2>(x, wb);
     const uint32_t tlo = t & 7, thi = t >> 3;
+    const uint32_t ba = tail_base_a(t), bb = tail_base_b(thi, tlo), bc = tail_base_c(t);
     tw_ct_tailB<5>(wb, ct, u0, q, thi);
     ct_stage<1>(x, wa);
 #pragma unroll
-    for (int k = 0; k < PT; k++) lds[swz_tail(t + NT * k)] = x[k];
+    for (int k = 0; k < PT; k++) lds[ba + tail_off_a(k)] = x[k];
     __syncthreads();
 #pragma unroll
-    for (int k = 0; k < PT; k++) x[k] = lds[swz_tail((thi << 8) | ((uint32_t)k << 3) | tlo)];
+    for (int k = 0; k < PT; k++) x[k] = lds[bb + tail_off_b(k)];
     tw_ct_tailB<6>(wa, ct, u0, q, thi);
     ct_stage<16>(x, wb);
     tw_ct_tailB<7>(wb, ct, u0, q, thi);
@@ -382,10 +404,10 @@ __global__ __launch_bounds__(NT, 2) void ct_tail_kernel(uint64_t* dst, size_t ds
     ct_stage<1>(x, wb);
     __syncthreads();
 #pragma unroll
-    for (int k = 0; k < PT; k++) lds[swz_tail((thi << 8) | ((uint32_t)k << 3) | tlo)] = x[k];
+    for (int k = 0; k < PT; k++) lds[bb + tail_off_b(k)] = x[k];
     __syncthreads();
 #pragma unroll
-    for (int k = 0; k < PT; k++) x[k] = lds[swz_tail(t * PT + k)];
+    for (int k = 0; k < PT; k++) x[k] = lds[bc + k];
     tw_ct_tailC<11>(wb, ct, u0, q, t);
     ct_stage<4>(x, wa);
     tw_ct_tailC<12>(wa, ct, u0, q, t);
@@ -393,11 +415,11 @@ __global__ __launch_bounds__(NT, 2) void ct_tail_kernel(uint64_t* dst, size_t ds
     ct_stage<1>(x, wa);
     __syncthreads();
 #pragma unroll
-    for (int k = 0; k < PT; k++) lds[swz_tail(t * PT + k)] = x[k];
+    for (int k = 0; k < PT; k++) lds[bc + k] = x[k];
     __syncthreads();
 #pragma unroll
     for (int k = 0; k < PT; k++) {
-        const uint64_t v = lds[swz_tail(t + NT * k)];
+        const uint64_t v = lds[ba + tail_off_a(k)];
         d[t + NT * k] = canon_out ? canon_u64(v) : v;
     }
 }
