@@ -361,10 +361,12 @@ def test_witness_commit_matches_oracle(bj, c, log_n, log_d, cap):
     eq(bj.field.to_host(ws.cap), ref["cap"])
 
 
-def test_commit_host_abi_matches(bj):
+@pytest.mark.parametrize("c,log_n,log_d,cap", [(5, 8, 2, 4), (70, 10, 1, 16), (64, 12, 2, 8), (33, 14, 3, 16)])
+def test_commit_host_abi_matches(bj, c, log_n, log_d, cap):
+    """bj_lde_commit_h: the column-chunked host pipeline (32-column chunks: one ragged, several
+    full, and a 1-column tail) equals the oracle's one-shot commit."""
     import ctypes
     from boojum_amd._lib import call
-    c, log_n, log_d, cap = 5, 8, 2, 4
     tr = O.synthetic_trace(c, log_n)
     nl = 1 << (log_n + log_d)
     lde = np.zeros((c, 1 << log_d, 1 << log_n), dtype=np.uint64)
@@ -373,7 +375,7 @@ def test_commit_host_abi_matches(bj):
     capo = np.zeros((cap, 4), dtype=np.uint64)
     p = lambda a: a.ctypes.data_as(ctypes.POINTER(ctypes.c_uint64))  # noqa: E731
     call("bj_lde_commit_h", p(np.ascontiguousarray(tr)), c, log_n, log_d, cap, p(lde), p(leaves), p(nodes), p(capo))
-    ref = O.lde_commit(tr, log_d, cap)
+    ref = O.lde_commit(tr, log_d, cap, threads=8)
     eq(lde, ref["lde"])
     eq(leaves, ref["leaves"])
     eq(nodes, ref["nodes"])
