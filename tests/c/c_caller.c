@@ -1,0 +1,222 @@
+/*
+ * c_caller.c -- a plain-C caller of the C ABI (include/boojum_mi355x.h), as a Rust prover's
+ * FFI would bind it: host Vecs in, no torch, no Python.  Test infrastructure (it also links the
+ * CPU oracle, oracle/liboracle.so, as the checker); built by tests/c/Makefile, run by
+ * tests/test_gpu_c_caller.py on the GPU box.
+ *
+ * Checks, each against the oracle restatement of the reference:
+ *   1. the per-column FFT seam the reference calls from rayon workers
+ *      (PrimeFieldLikeVectorized, field/traits/field_like.rs:111-162; fft/mod.rs:398-411,
+ *      464-491): twiddles, ifft_natural_to_natural, fft_natural_to_bitreversed with a coset,
+ *      distribute_powers -- called concurrently from T threads on distinct columns;
+ *   2. TreeHasher leaf/node (cs/oracle/mod.rs:141-168);
+ *   3. the whole witness commit through the host-buffer entry point bj_lde_commit_h
+ *      (prover.rs:313-353): LDE, leaves, nodes and cap bit-exact;
+ *   4. the error contract: a violated precondition (fft/mod.rs:399-402 asserts a power-of-two
+ *      length) returns BJ_EINVAL with a message, and the library keeps working.
+ *
+ * usage: c_caller LOG_N N_COLS LOG_LDE CAP THREADS      prints "c_caller ok ..." on success
+ */
+#include <pthread.h>
+#include <stdint.h>
+#include <stdio.h>
+#include <stdlib.h>
+#include <string.h>
+
+#include "boojum_mi355x.h"
+
+typedef uint64_t u64;
+#define GL_P 0xFFFFFFFF00000001ull
+
+/* oracle/boojum_oracle.c (the checker) */
+u64 bjo_domain_generator(uint32_t log_n);
+u64 bjo_gl_pow(u64 b, u64 e);
+void bjo_precompute_twiddles(uint32_t log_n, int inverse, u64* out);
+void bjo_distribute_powers(u64* a, size_t n, u64 element);
+void bjo_fft_natural_to_bitreversed(u64* a, size_t n, u64 coset, const u64* tw);
+void bjo_ifft_natural_to_natural(u64* a, size_t n, u64 coset, const u64* inv_tw);
+void bjo_hash_into_leaf(const u64* elems, size_t count, u64* out4);
+void bjo_hash_into_node(const u64* l, const u64* r, u64* out4);
+int bjo_lde_commit(u64* trace, uint32_t n_cols, uint32_t log_n, uint32_t log_d, uint32_t cap_size, u64* lde,
+                   u64* leaves, u64* nodes, u64* cap_out, int threads);
+
+static int failures = 0;
+#define CHECK(cond, ...)                      \
+    do {                                      \
+        if (!(cond)) {                        \
+            fprintf(stderr, "FAIL: " __VA_ARGS__); \
+            fprintf(stderr, "\n");            \
+            failures++;                       \
+        }                                     \
+    } while (0)
+
+/* SURVEY 8(d) synthetic trace: splitmix64(seed = 42 + c*n + r), reduced below p */
+static u64 splitmix64(u64 x) {
+    x += 0x9E3779B97F4A7C15ull;
+    x = (x ^ (x >> 30)) * 0xBF58476D1CE4E5B9ull;
+    x = (x ^ (x >> 27)) * 0x94D049BB133111EBull;
+    return x ^ (x >> 31);
+}
+
+static u64 canon(u64 x) { return x >= GL_P ? x - GL_P : x; }
+
+static int eq_canon(const u64* a, const u64* b, size_t n, size_t* where) {
+    for (size_t i = 0; i < n; i++)
+        if (canon(a[i]) != canon(b[i])) {
+            *where = i;
+            return 0;
+        }
+    return 1;
+}
+
+static void* xmalloc(size_t bytes) {
+    void* p = malloc(bytes ? bytes : 1);
+    if (!p) {
+        fprintf(stderr, "out of host memory\n");
+        exit(2);
+    }
+    return p;
+}
+
+/* ------------------------------------------------ 1. concurrent per-column FFT seam */
+
+typedef struct {
+    u64* cols;          /* n_cols x n, in place */
+    size_t n;
+    uint32_t first, count;
+    u64 coset;
+    int rc;
+} seam_job_t;
+
+/* utils.rs:295-304,363-379: one column per call from a worker thread, in place */
+static void* seam_worker(void* p) {
+    seam_job_t* j = (seam_job_t*)p;
+    j->rc = 0;
+    for (uint32_t c = j->first; c < j->first + j->count && j->rc == 0; c++) {
+        u64* col = j->cols + (size_t)c * j->n;
+        j->rc = bj_ifft_natural_to_natural_h(col, j->n, 1);
+        if (j->rc == 0) j->rc = bj_fft_natural_to_bitreversed_h(col, j->n, j->coset);
+    }
+    return NULL;
+}
+
+static void check_fft_seam(uint32_t log_n, uint32_t n_cols, int threads) {
+    size_t n = (size_t)1 << log_n;
+    u64* tw = xmalloc(8 * (n / 2));
+    u64* tw_ref = xmalloc(8 * (n / 2));
+    for (int inv = 0; inv < 2; inv++) {
+        CHECK(bj_precompute_twiddles_h(log_n, inv, tw) == BJ_OK, "bj_precompute_twiddles_h: %s", bj_last_error());
+        bjo_precompute_twiddles(log_n, inv, tw_ref);
+        size_t w = 0;
+        CHECK(eq_canon(tw, tw_ref, n / 2, &w), "twiddles (inverse=%d) differ at %zu", inv, w);
+    }
+    u64* cols = xmalloc(8 * n * n_cols);
+    u64* ref = xmalloc(8 * n * n_cols);
+    for (size_t i = 0; i < n * n_cols; i++) cols[i] = ref[i] = splitmix64(7 + i); /* non-canonical inputs too */
+    /* the LDE's coset for i = 1 of D = 2: 7 * w_{2n} (utils.rs:334-347) */
+    u64 coset = canon((u64)(((unsigned __int128)7 * bjo_gl_pow(bjo_domain_generator(log_n + 1), 1)) % GL_P));
+    pthread_t* th = xmalloc(sizeof(pthread_t) * threads);
+    seam_job_t* jobs = xmalloc(sizeof(seam_job_t) * threads);
+    uint32_t per = (n_cols + threads - 1) / threads;
+    for (int t = 0; t < threads; t++) {
+        uint32_t first = t * per < n_cols ? t * per : n_cols;
+        uint32_t count = first + per <= n_cols ? per : n_cols - first;
+        jobs[t] = (seam_job_t){cols, n, first, count, coset, 0};
+        pthread_create(&th[t], NULL, seam_worker, &jobs[t]);
+    }
+    for (int t = 0; t < threads; t++) {
+        pthread_join(th[t], NULL);
+        CHECK(jobs[t].rc == BJ_OK, "seam thread %d: rc %d (%s)", t, jobs[t].rc, bj_last_error());
+    }
+    bjo_precompute_twiddles(log_n, 1, tw_ref);
+    bjo_precompute_twiddles(log_n, 0, tw);
+    for (uint32_t c = 0; c < n_cols; c++) {
+        bjo_ifft_natural_to_natural(ref + (size_t)c * n, n, 1, tw_ref);
+        bjo_fft_natural_to_bitreversed(ref + (size_t)c * n, n, coset, tw);
+    }
+    size_t w = 0;
+    CHECK(eq_canon(cols, ref, n * n_cols, &w), "concurrent ifft+fft seam differs at %zu", w);
+    /* distribute_powers (fft/mod.rs:308-317) */
+    memcpy(cols, ref, 8 * n);
+    CHECK(bj_distribute_powers_h(cols, n, coset) == BJ_OK, "bj_distribute_powers_h: %s", bj_last_error());
+    bjo_distribute_powers(ref, n, coset);
+    CHECK(eq_canon(cols, ref, n, &w), "distribute_powers differs at %zu", w);
+    free(th); free(jobs); free(cols); free(ref); free(tw); free(tw_ref);
+}
+
+/* -------------------------------------------------------------- 2. TreeHasher */
+
+static void check_tree_hasher(void) {
+    u64 elems[19], got[4], want[4];
+    for (int i = 0; i < 19; i++) elems[i] = splitmix64(100 + i);
+    for (size_t len = 0; len <= 19; len++) {  /* every sponge padding case up to 2 blocks + 3 */
+        CHECK(bj_hash_into_leaf_h(elems, len, got) == BJ_OK, "bj_hash_into_leaf_h: %s", bj_last_error());
+        bjo_hash_into_leaf(elems, len, want);
+        size_t w = 0;
+        CHECK(eq_canon(got, want, 4, &w), "leaf of %zu elements differs", len);
+    }
+    CHECK(bj_hash_into_node_h(elems, elems + 4, got) == BJ_OK, "bj_hash_into_node_h: %s", bj_last_error());
+    bjo_hash_into_node(elems, elems + 4, want);
+    size_t w = 0;
+    CHECK(eq_canon(got, want, 4, &w), "node hash differs");
+}
+
+/* ------------------------------------------------------ 3. whole witness commit */
+
+static void check_commit(uint32_t log_n, uint32_t n_cols, uint32_t log_lde, uint32_t cap, int threads,
+                         u64* cap_out) {
+    size_t n = (size_t)1 << log_n, nl = n << log_lde, n_nodes = nl - cap;
+    u64* trace = xmalloc(8 * n * n_cols);
+    for (uint32_t c = 0; c < n_cols; c++)
+        for (size_t r = 0; r < n; r++) trace[(size_t)c * n + r] = canon(splitmix64(42 + (u64)c * n + r));
+    u64* lde = xmalloc(8 * nl * n_cols), *leaves = xmalloc(32 * nl), *nodes = xmalloc(32 * n_nodes);
+    int rc = bj_lde_commit_h(trace, n_cols, log_n, log_lde, cap, lde, leaves, nodes, cap_out);
+    CHECK(rc == BJ_OK, "bj_lde_commit_h: rc %d (%s)", rc, bj_last_error());
+    u64* r_lde = xmalloc(8 * nl * n_cols), *r_leaves = xmalloc(32 * nl), *r_nodes = xmalloc(32 * n_nodes);
+    u64 r_cap[4 * 4096];
+    bjo_lde_commit(trace, n_cols, log_n, log_lde, cap, r_lde, r_leaves, r_nodes, r_cap, threads);
+    size_t w = 0;
+    CHECK(eq_canon(lde, r_lde, nl * n_cols, &w), "LDE differs at %zu", w);
+    CHECK(eq_canon(leaves, r_leaves, 4 * nl, &w), "leaves differ at %zu", w);
+    CHECK(eq_canon(nodes, r_nodes, 4 * n_nodes, &w), "nodes differ at %zu", w);
+    CHECK(eq_canon(cap_out, r_cap, 4 * cap, &w), "cap differs at %zu", w);
+    free(trace); free(lde); free(leaves); free(nodes); free(r_lde); free(r_leaves); free(r_nodes);
+}
+
+/* ------------------------------------------------------------ 4. error contract */
+
+static void check_errors(void) {
+    u64 col[12] = {0};
+    CHECK(bj_fft_natural_to_bitreversed_h(col, 12, 1) == BJ_EINVAL, "length 12 must be rejected");
+    CHECK(strlen(bj_last_error()) > 0, "no error message after BJ_EINVAL");
+    u64 st[12] = {0};
+    CHECK(bj_poseidon2_permute_h(st) == BJ_OK, "library unusable after an error: %s", bj_last_error());
+}
+
+int main(int argc, char** argv) {
+    if (argc != 6) {
+        fprintf(stderr, "usage: %s LOG_N N_COLS LOG_LDE CAP THREADS\n", argv[0]);
+        return 2;
+    }
+    uint32_t log_n = atoi(argv[1]), n_cols = atoi(argv[2]), log_lde = atoi(argv[3]), cap = atoi(argv[4]);
+    int threads = atoi(argv[5]);
+    if (cap == 0 || cap > 4096 || (cap & (cap - 1)) || threads < 1) {
+        fprintf(stderr, "cap must be a power of two <= 4096, threads >= 1\n");
+        return 2;
+    }
+    fprintf(stderr, "abi %u.%u\n", bj_abi_version() >> 16, bj_abi_version() & 0xffff);
+    check_fft_seam(log_n, n_cols, threads);
+    check_tree_hasher();
+    u64 cap_out[4 * 4096];
+    check_commit(log_n, n_cols, log_lde, cap, threads, cap_out);
+    check_errors();
+    if (failures) {
+        fprintf(stderr, "%d check(s) failed\n", failures);
+        return 1;
+    }
+    printf("c_caller ok: 2^%u x %u, LDE x%u, cap %u, %d seam threads; cap[0] = %016llx %016llx %016llx %016llx\n",
+           log_n, n_cols, 1u << log_lde, cap, threads, (unsigned long long)canon(cap_out[0]),
+           (unsigned long long)canon(cap_out[1]), (unsigned long long)canon(cap_out[2]),
+           (unsigned long long)canon(cap_out[3]));
+    return 0;
+}

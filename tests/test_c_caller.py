@@ -1,0 +1,40 @@
+"""The C ABI driven from plain C (tests/c/c_caller.c), the way a Rust prover's FFI binds it:
+host buffers, per-column FFT seam called concurrently from threads, TreeHasher, the
+host-buffer witness commit and the error contract, each checked against the CPU oracle.
+
+The non-GPU test only checks that the caller links against the product library; the GPU
+tests run it (C1's geometry at two thread counts, a ragged column count, LDE x8)."""
+import os
+import subprocess
+
+import pytest
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+BIN = os.path.join(ROOT, "tests", "c", "c_caller")
+
+
+def _need_bin():
+    if not os.path.exists(BIN):
+        pytest.fail("tests/c/c_caller is not built (run __graft_entry__.build())")
+
+
+def test_c_caller_links_the_product_library():
+    _need_bin()
+    out = subprocess.run(["ldd", BIN], check=True, capture_output=True, text=True).stdout
+    lines = {ln.split()[0]: ln for ln in out.splitlines() if "=>" in ln}
+    assert "libboojum_mi355x.so" in lines and "not found" not in lines["libboojum_mi355x.so"], out
+    assert "liboracle.so" in lines and "not found" not in lines["liboracle.so"], out
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("log_n,cols,log_lde,cap,threads", [
+    (16, 32, 1, 16, 8),    # C1, seam called from 8 threads
+    (12, 19, 2, 8, 3),     # ragged leaf length (19 = 2 sponge blocks + 3)
+    (10, 8, 3, 32, 1),     # LDE x8, cap 32
+])
+def test_c_caller(log_n, cols, log_lde, cap, threads):
+    _need_bin()
+    r = subprocess.run([BIN, str(log_n), str(cols), str(log_lde), str(cap), str(threads)], capture_output=True,
+                       text=True, timeout=120)
+    assert r.returncode == 0, r.stdout + r.stderr
+    assert "c_caller ok" in r.stdout, r.stdout
