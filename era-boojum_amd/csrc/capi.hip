@@ -230,10 +230,37 @@ uint64_t lde_coset(uint32_t log_n, uint32_t log_d, uint32_t i) {
     return gl::canon(gl::mul(gl::pow(g, gl::bitrev32(i, log_d)), gl::GENERATOR));
 }
 
-// Device buffer RAII for the *_h entry points.
+// The *_h entry points run on a stream of their own per calling thread and device (created
+// once; stream creation costs milliseconds on ROCm), with stream-ordered device buffers and
+// explicit copies + synchronisation.  Nothing of theirs touches the legacy null stream, which
+// every host thread shares.
+int seam_stream(hipStream_t* out) {
+    thread_local std::map<int, hipStream_t> tl;
+    int dev = 0;
+    HIP_TRY(hipGetDevice(&dev), "hipGetDevice");
+    auto it = tl.find(dev);
+    if (it == tl.end()) {
+        hipStream_t st;
+        HIP_TRY(hipStreamCreateWithFlags(&st, hipStreamNonBlocking), "hipStreamCreate");
+        // keep the stream-ordered pool's freed memory mapped (as bj_lde_commit_h does), so a
+        // per-column call does not re-map its buffers after every synchronisation
+        hipMemPool_t pool;
+        HIP_TRY(hipDeviceGetDefaultMemPool(&pool, dev), "hipDeviceGetDefaultMemPool");
+        uint64_t keep = UINT64_MAX;
+        HIP_TRY(hipMemPoolSetAttribute(pool, hipMemPoolAttrReleaseThreshold, &keep), "hipMemPoolSetAttribute");
+        it = tl.emplace(dev, st).first;
+    }
+    *out = it->second;
+    return BJ_OK;
+}
+
+// Stream-ordered device buffer RAII for the *_h entry points.
 struct DBuf {
     uint64_t* p = nullptr;
-    ~DBuf() { if (p) (void)hipFree(p); }
+    hipStream_t st = nullptr;
+    explicit DBuf(hipStream_t s) : st(s) {}
+    hipError_t alloc(size_t bytes) { return hipMallocAsync((void**)&p, bytes ? bytes : 8, st); }
+    ~DBuf() { if (p) (void)hipFreeAsync(p, st); }
 };
 
 }  // namespace
@@ -351,7 +378,10 @@ int bj_precompute_twiddles_h(uint32_t log_n, int inverse, uint64_t* out_h) {
     if (log_n == 0) return fail(BJ_EINVAL, "twiddles need n >= 2");
     const uint64_t* t;
     if (int r = get_twiddles(log_n, inverse != 0, &t)) return r;
-    HIP_TRY(hipMemcpy(out_h, t, ((size_t)1 << (log_n - 1)) * 8, hipMemcpyDeviceToHost), "memcpy");
+    hipStream_t st;
+    if (int r = seam_stream(&st)) return r;
+    HIP_TRY(hipMemcpyAsync(out_h, t, ((size_t)1 << (log_n - 1)) * 8, hipMemcpyDeviceToHost, st), "memcpy");
+    HIP_TRY(hipStreamSynchronize(st), "sync");
     return BJ_OK;
 }
 
@@ -661,108 +691,135 @@ int bj_lde_commit_d(const uint64_t* trace, uint32_t n_cols, size_t trace_stride,
 
 // --------------------------------------------------------- host-pointer seam
 
+#define SEAM_BEGIN            \
+    hipStream_t st;           \
+    if (int r_ = seam_stream(&st)) return r_
+#define H2D(dst, src, bytes) HIP_TRY(hipMemcpyAsync(dst, src, bytes, hipMemcpyHostToDevice, st), "memcpy")
+#define D2H(dst, src, bytes) HIP_TRY(hipMemcpyAsync(dst, src, bytes, hipMemcpyDeviceToHost, st), "memcpy")
+#define SEAM_END HIP_TRY(hipStreamSynchronize(st), "sync")
+
 int bj_distribute_powers_h(uint64_t* col, size_t len, uint64_t element) {
     uint32_t log_n;
     if (int r = log2_exact(len, &log_n)) return r;
-    DBuf d;
-    HIP_TRY(hipMalloc(&d.p, len * 8), "hipMalloc");
-    HIP_TRY(hipMemcpy(d.p, col, len * 8, hipMemcpyHostToDevice), "memcpy");
-    if (int r = bj_distribute_powers_d(d.p, 1, len, log_n, element, nullptr)) return r;
-    HIP_TRY(hipMemcpy(col, d.p, len * 8, hipMemcpyDeviceToHost), "memcpy");
+    SEAM_BEGIN;
+    DBuf d(st);
+    HIP_TRY(d.alloc(len * 8), "hipMallocAsync");
+    H2D(d.p, col, len * 8);
+    if (int r = bj_distribute_powers_d(d.p, 1, len, log_n, element, st)) return r;
+    D2H(col, d.p, len * 8);
+    SEAM_END;
     return BJ_OK;
 }
 
 int bj_fft_natural_to_bitreversed_h(uint64_t* col, size_t len, uint64_t coset) {
     uint32_t log_n;
     if (int r = log2_exact(len, &log_n)) return r;
-    DBuf d;
-    HIP_TRY(hipMalloc(&d.p, len * 8), "hipMalloc");
-    HIP_TRY(hipMemcpy(d.p, col, len * 8, hipMemcpyHostToDevice), "memcpy");
-    if (int r = bj_fft_natural_to_bitreversed_d(d.p, 1, len, log_n, coset, nullptr, nullptr)) return r;
-    HIP_TRY(hipMemcpy(col, d.p, len * 8, hipMemcpyDeviceToHost), "memcpy");
+    SEAM_BEGIN;
+    DBuf d(st);
+    HIP_TRY(d.alloc(len * 8), "hipMallocAsync");
+    H2D(d.p, col, len * 8);
+    if (int r = bj_fft_natural_to_bitreversed_d(d.p, 1, len, log_n, coset, nullptr, st)) return r;
+    D2H(col, d.p, len * 8);
+    SEAM_END;
     return BJ_OK;
 }
 
 int bj_ifft_natural_to_natural_h(uint64_t* col, size_t len, uint64_t coset) {
     uint32_t log_n;
     if (int r = log2_exact(len, &log_n)) return r;
-    DBuf d;
-    HIP_TRY(hipMalloc(&d.p, len * 8), "hipMalloc");
-    HIP_TRY(hipMemcpy(d.p, col, len * 8, hipMemcpyHostToDevice), "memcpy");
-    if (int r = bj_ifft_natural_to_natural_d(d.p, 1, len, log_n, coset, nullptr, nullptr)) return r;
-    HIP_TRY(hipMemcpy(col, d.p, len * 8, hipMemcpyDeviceToHost), "memcpy");
+    SEAM_BEGIN;
+    DBuf d(st);
+    HIP_TRY(d.alloc(len * 8), "hipMallocAsync");
+    H2D(d.p, col, len * 8);
+    if (int r = bj_ifft_natural_to_natural_d(d.p, 1, len, log_n, coset, nullptr, st)) return r;
+    D2H(col, d.p, len * 8);
+    SEAM_END;
     return BJ_OK;
 }
 
 int bj_poseidon2_permute_h(uint64_t* state12) {
-    DBuf d;
-    HIP_TRY(hipMalloc(&d.p, 96), "hipMalloc");
-    HIP_TRY(hipMemcpy(d.p, state12, 96, hipMemcpyHostToDevice), "memcpy");
-    if (int r = bj_poseidon2_permute_d(d.p, 1, nullptr)) return r;
-    HIP_TRY(hipMemcpy(state12, d.p, 96, hipMemcpyDeviceToHost), "memcpy");
+    SEAM_BEGIN;
+    DBuf d(st);
+    HIP_TRY(d.alloc(96), "hipMallocAsync");
+    H2D(d.p, state12, 96);
+    if (int r = bj_poseidon2_permute_d(d.p, 1, st)) return r;
+    D2H(state12, d.p, 96);
+    SEAM_END;
     return BJ_OK;
 }
 
 int bj_hash_into_leaf_h(const uint64_t* elems, size_t n_elems, uint64_t* out4) {
-    DBuf d, o;
-    HIP_TRY(hipMalloc(&d.p, (n_elems ? n_elems : 1) * 8), "hipMalloc");
-    HIP_TRY(hipMalloc(&o.p, 32), "hipMalloc");
-    if (n_elems) HIP_TRY(hipMemcpy(d.p, elems, n_elems * 8, hipMemcpyHostToDevice), "memcpy");
-    if (int r = bj_merkle_leaves_d(d.p, (uint32_t)n_elems, 1, 1, o.p, nullptr)) return r;
-    HIP_TRY(hipMemcpy(out4, o.p, 32, hipMemcpyDeviceToHost), "memcpy");
+    SEAM_BEGIN;
+    DBuf d(st), o(st);
+    HIP_TRY(d.alloc(n_elems * 8), "hipMallocAsync");
+    HIP_TRY(o.alloc(32), "hipMallocAsync");
+    if (n_elems) H2D(d.p, elems, n_elems * 8);
+    if (int r = bj_merkle_leaves_d(d.p, (uint32_t)n_elems, 1, 1, o.p, st)) return r;
+    D2H(out4, o.p, 32);
+    SEAM_END;
     return BJ_OK;
 }
 
 int bj_hash_into_node_h(const uint64_t* left4, const uint64_t* right4, uint64_t* out4) {
-    DBuf d;
-    HIP_TRY(hipMalloc(&d.p, 96), "hipMalloc");
-    HIP_TRY(hipMemcpy(d.p, left4, 32, hipMemcpyHostToDevice), "memcpy");
-    HIP_TRY(hipMemcpy(d.p + 4, right4, 32, hipMemcpyHostToDevice), "memcpy");
-    if (int r = bj_merkle_nodes_d(d.p, 2, 1, d.p + 8, nullptr)) return r;
-    HIP_TRY(hipMemcpy(out4, d.p + 8, 32, hipMemcpyDeviceToHost), "memcpy");
+    SEAM_BEGIN;
+    DBuf d(st);
+    HIP_TRY(d.alloc(96), "hipMallocAsync");
+    H2D(d.p, left4, 32);
+    H2D(d.p + 4, right4, 32);
+    if (int r = bj_merkle_nodes_d(d.p, 2, 1, d.p + 8, st)) return r;
+    D2H(out4, d.p + 8, 32);
+    SEAM_END;
     return BJ_OK;
 }
 
 int bj_blake2s_leaf_h(const uint64_t* elems, size_t n_elems, uint64_t* out4) {
     if (n_elems > 0xFFFFFFFFull) return fail(BJ_EINVAL, "leaf too long");
-    DBuf d, o;
-    HIP_TRY(hipMalloc(&d.p, (n_elems ? n_elems : 1) * 8), "hipMalloc");
-    HIP_TRY(hipMalloc(&o.p, 32), "hipMalloc");
-    if (n_elems) HIP_TRY(hipMemcpy(d.p, elems, n_elems * 8, hipMemcpyHostToDevice), "memcpy");
-    HIP_TRY(bj::launch_b2s_words(d.p, (uint32_t)n_elems, o.p, nullptr), "blake2s");
-    HIP_TRY(hipMemcpy(out4, o.p, 32, hipMemcpyDeviceToHost), "memcpy");
+    SEAM_BEGIN;
+    DBuf d(st), o(st);
+    HIP_TRY(d.alloc(n_elems * 8), "hipMallocAsync");
+    HIP_TRY(o.alloc(32), "hipMallocAsync");
+    if (n_elems) H2D(d.p, elems, n_elems * 8);
+    HIP_TRY(bj::launch_b2s_words(d.p, (uint32_t)n_elems, o.p, st), "blake2s");
+    D2H(out4, o.p, 32);
+    SEAM_END;
     return BJ_OK;
 }
 
 int bj_blake2s_node_h(const uint64_t* left4, const uint64_t* right4, uint64_t* out4) {
-    DBuf d;
-    HIP_TRY(hipMalloc(&d.p, 96), "hipMalloc");
-    HIP_TRY(hipMemcpy(d.p, left4, 32, hipMemcpyHostToDevice), "memcpy");
-    HIP_TRY(hipMemcpy(d.p + 4, right4, 32, hipMemcpyHostToDevice), "memcpy");
-    if (int r = bj_blake2s_nodes_d(d.p, 2, 1, d.p + 8, nullptr)) return r;
-    HIP_TRY(hipMemcpy(out4, d.p + 8, 32, hipMemcpyDeviceToHost), "memcpy");
+    SEAM_BEGIN;
+    DBuf d(st);
+    HIP_TRY(d.alloc(96), "hipMallocAsync");
+    H2D(d.p, left4, 32);
+    H2D(d.p + 4, right4, 32);
+    if (int r = bj_blake2s_nodes_d(d.p, 2, 1, d.p + 8, st)) return r;
+    D2H(out4, d.p + 8, 32);
+    SEAM_END;
     return BJ_OK;
 }
 
 int bj_keccak256_leaf_h(const uint64_t* elems, size_t n_elems, uint64_t* out4) {
     if (n_elems > 0xFFFFFFFFull) return fail(BJ_EINVAL, "leaf too long");
-    DBuf d, o;
-    HIP_TRY(hipMalloc(&d.p, (n_elems ? n_elems : 1) * 8), "hipMalloc");
-    HIP_TRY(hipMalloc(&o.p, 32), "hipMalloc");
-    if (n_elems) HIP_TRY(hipMemcpy(d.p, elems, n_elems * 8, hipMemcpyHostToDevice), "memcpy");
+    SEAM_BEGIN;
+    DBuf d(st), o(st);
+    HIP_TRY(d.alloc(n_elems * 8), "hipMallocAsync");
+    HIP_TRY(o.alloc(32), "hipMallocAsync");
+    if (n_elems) H2D(d.p, elems, n_elems * 8);
     // the elements as n_elems one-row columns of one leaf
-    HIP_TRY(bj::launch_kc_leaves(d.p, 1, (uint32_t)n_elems, 1, o.p, nullptr), "keccak256");
-    HIP_TRY(hipMemcpy(out4, o.p, 32, hipMemcpyDeviceToHost), "memcpy");
+    HIP_TRY(bj::launch_kc_leaves(d.p, 1, (uint32_t)n_elems, 1, o.p, st), "keccak256");
+    D2H(out4, o.p, 32);
+    SEAM_END;
     return BJ_OK;
 }
 
 int bj_keccak256_node_h(const uint64_t* left4, const uint64_t* right4, uint64_t* out4) {
-    DBuf d;
-    HIP_TRY(hipMalloc(&d.p, 96), "hipMalloc");
-    HIP_TRY(hipMemcpy(d.p, left4, 32, hipMemcpyHostToDevice), "memcpy");
-    HIP_TRY(hipMemcpy(d.p + 4, right4, 32, hipMemcpyHostToDevice), "memcpy");
-    if (int r = bj_keccak256_nodes_d(d.p, 2, 1, d.p + 8, nullptr)) return r;
-    HIP_TRY(hipMemcpy(out4, d.p + 8, 32, hipMemcpyDeviceToHost), "memcpy");
+    SEAM_BEGIN;
+    DBuf d(st);
+    HIP_TRY(d.alloc(96), "hipMallocAsync");
+    H2D(d.p, left4, 32);
+    H2D(d.p + 4, right4, 32);
+    if (int r = bj_keccak256_nodes_d(d.p, 2, 1, d.p + 8, st)) return r;
+    D2H(out4, d.p + 8, 32);
+    SEAM_END;
     return BJ_OK;
 }
 

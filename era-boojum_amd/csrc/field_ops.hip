@@ -21,7 +21,10 @@ __global__ __launch_bounds__(256) void gl_op_kernel(int op, const uint64_t* __re
         case 1: glasm::add_x1(x0, x1, y0, y1, z0, z1); break;
         case 2: glasm::sub_x1(x0, x1, y0, y1, z0, z1); break;
         case 3: {  // limb reduction: L = a (< 2^63), H = b (< 2^63 with hi word < 2^31)
-            glasm::reduce_x1(x, y0, y1, z0, z1);
+            uint64_t z;
+            glasm::reduce_x1(x, y0, y1, z);
+            z0 = (uint32_t)z;
+            z1 = (uint32_t)(z >> 32);
             break;
         }
         default: z0 = x0; z1 = x1; break;  // 4: canonicalise a

@@ -45,22 +45,24 @@ __device__ __forceinline__ void split2(uint64_t x, uint32_t& lo, uint32_t& hi) {
 }
 __device__ __forceinline__ uint64_t join2(uint32_t lo, uint32_t hi) { return ((uint64_t)hi << 32) | lo; }
 
-// CT butterflies on four pairs: t = c * mu; (a, c) <- (a + t, a - t) in place
-// (glasm::ct_bfly_x4: t canonicalised, then single-correction subtract and add).
+// CT butterflies on four pairs: t = c * mu; (a, c) <- (a + t, a - t)
+// (glasm::ct_bfly_x4: t canonicalised, then one correcting 64-bit mad per output).
 __device__ __forceinline__ void ct_bfly_x4(uint64_t& xa0, uint64_t& xc0, uint64_t& xa1, uint64_t& xc1,
                                            uint64_t& xa2, uint64_t& xc2, uint64_t& xa3, uint64_t& xc3, uint64_t w0,
                                            uint64_t w1, uint64_t w2, uint64_t w3) {
-    uint32_t a0[4], a1[4], c0[4], c1[4], v0[4], v1[4];
-    split2(xa0, a0[0], a1[0]); split2(xc0, c0[0], c1[0]); split2(w0, v0[0], v1[0]);
-    split2(xa1, a0[1], a1[1]); split2(xc1, c0[1], c1[1]); split2(w1, v0[1], v1[1]);
-    split2(xa2, a0[2], a1[2]); split2(xc2, c0[2], c1[2]); split2(w2, v0[2], v1[2]);
-    split2(xa3, a0[3], a1[3]); split2(xc3, c0[3], c1[3]); split2(w3, v0[3], v1[3]);
-    glasm::ct_bfly_x4(a0[0], a1[0], c0[0], c1[0], v0[0], v1[0], a0[1], a1[1], c0[1], c1[1], v0[1], v1[1],
-                      a0[2], a1[2], c0[2], c1[2], v0[2], v1[2], a0[3], a1[3], c0[3], c1[3], v0[3], v1[3]);
-    xa0 = join2(a0[0], a1[0]); xc0 = join2(c0[0], c1[0]);
-    xa1 = join2(a0[1], a1[1]); xc1 = join2(c0[1], c1[1]);
-    xa2 = join2(a0[2], a1[2]); xc2 = join2(c0[2], c1[2]);
-    xa3 = join2(a0[3], a1[3]); xc3 = join2(c0[3], c1[3]);
+    uint64_t A[4], C[4];
+    glasm::ct_bfly_x4((uint32_t)xa0, (uint32_t)(xa0 >> 32), (uint32_t)xc0, (uint32_t)(xc0 >> 32), (uint32_t)w0,
+                      (uint32_t)(w0 >> 32), A[0], C[0],
+                      (uint32_t)xa1, (uint32_t)(xa1 >> 32), (uint32_t)xc1, (uint32_t)(xc1 >> 32), (uint32_t)w1,
+                      (uint32_t)(w1 >> 32), A[1], C[1],
+                      (uint32_t)xa2, (uint32_t)(xa2 >> 32), (uint32_t)xc2, (uint32_t)(xc2 >> 32), (uint32_t)w2,
+                      (uint32_t)(w2 >> 32), A[2], C[2],
+                      (uint32_t)xa3, (uint32_t)(xa3 >> 32), (uint32_t)xc3, (uint32_t)(xc3 >> 32), (uint32_t)w3,
+                      (uint32_t)(w3 >> 32), A[3], C[3]);
+    xa0 = A[0]; xc0 = C[0];
+    xa1 = A[1]; xc1 = C[1];
+    xa2 = A[2]; xc2 = C[2];
+    xa3 = A[3]; xc3 = C[3];
 }
 
 __device__ __forceinline__ void mul4_by(uint64_t& x0, uint64_t& x1, uint64_t& x2, uint64_t& x3, uint64_t k) {

@@ -13,7 +13,7 @@
 // * state element = (lo, hi) 32-bit halves of a u64 representative, one permutation per lane;
 // * linear layers run on "limbs": L = sum c_j lo_j and H = sum c_j hi_j in 64-bit lanes,
 //   so a linear combination never carries (coefficients here stay < 2^16); the round
-//   constant is added into the limbs, and one 5-instruction reduction
+//   constant is added into the limbs, and one 4-instruction reduction
 //   (glasm::reduce_xN) turns (L, H) back into a u64 per element;
 // * S-box multiplies are the interleaved inline-asm products of gl_asm.hpp.
 #pragma once
@@ -101,15 +101,24 @@ __device__ __forceinline__ void mds_ext_limbs(const uint32_t* v, uint64_t* X) {
     }
 }
 
-// (L, H) -> reduced (lo, hi) for all 12 elements.
+__device__ __forceinline__ void split(uint64_t z, uint32_t& lo, uint32_t& hi) {
+    lo = (uint32_t)z;
+    hi = (uint32_t)(z >> 32);
+}
+
+// (L, H) -> reduced (lo, hi) for all 12 elements.  The reductions write 64-bit register pairs;
+// lo / hi are their halves (sub-registers, no moves).
 __device__ __forceinline__ void reduce12(const uint64_t* L, const uint64_t* H, uint32_t* lo, uint32_t* hi) {
 #pragma unroll
     for (int q = 0; q < 3; q++) {
         const int i = 4 * q;
-        glasm::reduce_x4(L[i], (uint32_t)H[i], (uint32_t)(H[i] >> 32), lo[i], hi[i],
-                         L[i + 1], (uint32_t)H[i + 1], (uint32_t)(H[i + 1] >> 32), lo[i + 1], hi[i + 1],
-                         L[i + 2], (uint32_t)H[i + 2], (uint32_t)(H[i + 2] >> 32), lo[i + 2], hi[i + 2],
-                         L[i + 3], (uint32_t)H[i + 3], (uint32_t)(H[i + 3] >> 32), lo[i + 3], hi[i + 3]);
+        uint64_t z[4];
+        glasm::reduce_x4(L[i], (uint32_t)H[i], (uint32_t)(H[i] >> 32), z[0],
+                         L[i + 1], (uint32_t)H[i + 1], (uint32_t)(H[i + 1] >> 32), z[1],
+                         L[i + 2], (uint32_t)H[i + 2], (uint32_t)(H[i + 2] >> 32), z[2],
+                         L[i + 3], (uint32_t)H[i + 3], (uint32_t)(H[i + 3] >> 32), z[3]);
+#pragma unroll
+        for (int j = 0; j < 4; j++) split(z[j], lo[i + j], hi[i + j]);
     }
 }
 
@@ -129,41 +138,63 @@ __device__ __forceinline__ void full_round(State& s, uint64_t* L, uint64_t* H, i
     mds_ext_limbs(s.hi, H);
 }
 
-// Partial-round S-box on a reduced s0: s0 += RC_r, s0 = s0^7.
-__device__ __forceinline__ void partial_sbox(State& s, int r) {
-    uint64_t L0 = (uint64_t)s.lo[0] + RCL.lo[r][0];
-    uint64_t H0 = (uint64_t)s.hi[0] + RCL.hi[r][0];
-    glasm::reduce_x1(L0, (uint32_t)H0, (uint32_t)(H0 >> 32), s.lo[0], s.hi[0]);
-    sbox_x1(s.lo[0], s.hi[0]);
+// lo + b as a 64-bit limb in one v_mad_u64_u32 (lo * 1 + b): no zero-extended register pair
+// for lo.  b is wave-uniform (a round-constant limb in an SGPR pair).
+__device__ __forceinline__ uint64_t add_lo_u64(uint32_t lo, uint64_t b) {
+    uint64_t r;
+    asm volatile("v_mad_u64_u32 %0, vcc, %1, 1, %2" : "=v"(r) : "v"(lo), "s"(b) : "vcc");
+    return r;
 }
 
-// Two partial rounds r, r + 1.  M_I of round r leaves elements 1..11 as unreduced limbs
-// (< 2^46.6); only s0, the next S-box input, is reduced.  Round r + 1's M_I consumes the limbs
-// (sums < 2^50.2, shifted terms < 2^61) and reduces every element.  Same field values as two
-// reduced rounds (glasm::mi_layer_a / mi_layer_b, tools/gen_gl_asm.py).
-__device__ __forceinline__ void partial_round_pair(State& s, int r) {
-    uint64_t L[12], H[12];
-    partial_sbox(s, r);
-    glasm::mi_layer_a(s.lo, s.hi, L, H);
-    partial_sbox(s, r + 1);
-    glasm::mi_layer_b(s.lo, s.hi, L, H);
+// Partial-round S-box on a reduced z: z += RC_r, z^7 as 32-bit halves (lo, hi).
+__device__ __forceinline__ void partial_sbox(uint64_t z, int r, uint32_t& lo, uint32_t& hi) {
+    const uint64_t L0 = add_lo_u64((uint32_t)z, RCL.lo[r][0]);
+    const uint64_t H0 = add_lo_u64((uint32_t)(z >> 32), RCL.hi[r][0]);
+    uint64_t y;
+    glasm::reduce_x1(L0, (uint32_t)H0, (uint32_t)(H0 >> 32), y);
+    split(y, lo, hi);
+    sbox_x1(lo, hi);
+}
+
+// Two partial rounds r, r + 1 on the state as 64-bit register pairs Z (the reductions' own
+// output pairs, so the loop carries no 32-bit copies).  M_I of round r leaves elements 1..11
+// as unreduced limbs (< 2^46.6); only s0, the next S-box input, is reduced.  Round r + 1's M_I
+// consumes the limbs (sums < 2^50.2, shifted terms < 2^61) and reduces every element.  Same
+// field values as two reduced rounds (glasm::mi_layer_a / mi_layer_b, tools/gen_gl_asm.py).
+__device__ __forceinline__ void partial_round_pair(uint64_t* Z, int r) {
+    uint64_t L[12], H[12], z0;
+    uint32_t lo[12], hi[12];
+#pragma unroll
+    for (int i = 1; i < 12; i++) split(Z[i], lo[i], hi[i]);
+    partial_sbox(Z[0], r, lo[0], hi[0]);
+    glasm::mi_layer_a(lo, hi, L, H, z0);
+    uint32_t lo0, hi0;
+    partial_sbox(z0, r + 1, lo0, hi0);
+    glasm::mi_layer_b(lo0, hi0, L, H, Z);
 }
 
 // The permutation (state_generic_impl.rs:221-236): MDS; 4 x (RC, S-box, MDS);
 // 22 partial rounds; 4 x (RC, S-box, MDS).
 __device__ __forceinline__ void permute(State& s) {
-    uint64_t L[12], H[12];
+    uint64_t L[12], H[12], Z[12];
     mds_ext_limbs(s.lo, L);
     mds_ext_limbs(s.hi, H);
 #pragma unroll 1
     for (int r = 0; r < 4; r++) full_round(s, L, H, r);
-    reduce12(L, H, s.lo, s.hi);
+#pragma unroll
+    for (int q = 0; q < 3; q++) {
+        const int i = 4 * q;
+        glasm::reduce_x4(L[i], (uint32_t)H[i], (uint32_t)(H[i] >> 32), Z[i],
+                         L[i + 1], (uint32_t)H[i + 1], (uint32_t)(H[i + 1] >> 32), Z[i + 1],
+                         L[i + 2], (uint32_t)H[i + 2], (uint32_t)(H[i + 2] >> 32), Z[i + 2],
+                         L[i + 3], (uint32_t)H[i + 3], (uint32_t)(H[i + 3] >> 32), Z[i + 3]);
+    }
 #pragma unroll 1
-    for (int r = 4; r < 26; r += 2) partial_round_pair(s, r);
+    for (int r = 4; r < 26; r += 2) partial_round_pair(Z, r);
 #pragma unroll
     for (int i = 0; i < 12; i++) {
-        L[i] = s.lo[i];
-        H[i] = s.hi[i];
+        L[i] = (uint32_t)Z[i];
+        H[i] = Z[i] >> 32;
     }
 #pragma unroll 1
     for (int r = 26; r < 30; r++) full_round(s, L, H, r);

@@ -2,13 +2,14 @@
  * c_caller.c -- a plain-C caller of the C ABI (include/boojum_mi355x.h), as a Rust prover's
  * FFI would bind it: host Vecs in, no torch, no Python.  Test infrastructure (it also links the
  * CPU oracle, oracle/liboracle.so, as the checker); built by tests/c/Makefile, run by
- * tests/test_gpu_c_caller.py on the GPU box.
+ * tests/test_c_caller.py on the GPU box.
  *
  * Checks, each against the oracle restatement of the reference:
  *   1. the per-column FFT seam the reference calls from rayon workers
  *      (PrimeFieldLikeVectorized, field/traits/field_like.rs:111-162; fft/mod.rs:398-411,
  *      464-491): twiddles, ifft_natural_to_natural, fft_natural_to_bitreversed with a coset,
- *      distribute_powers -- called concurrently from T threads on distinct columns;
+ *      distribute_powers -- called concurrently from T threads on distinct columns, three rounds
+ *      (an earlier null-stream version of the seam returned a stale column about every other run);
  *   2. TreeHasher leaf/node (cs/oracle/mod.rs:141-168);
  *   3. the whole witness commit through the host-buffer entry point bj_lde_commit_h
  *      (prover.rs:313-353): LDE, leaves, nodes and cap bit-exact;
@@ -205,7 +206,7 @@ int main(int argc, char** argv) {
         return 2;
     }
     fprintf(stderr, "abi %u.%u\n", bj_abi_version() >> 16, bj_abi_version() & 0xffff);
-    check_fft_seam(log_n, n_cols, threads);
+    for (int round = 0; round < 3; round++) check_fft_seam(log_n, n_cols, threads);
     check_tree_hasher();
     u64 cap_out[4 * 4096];
     check_commit(log_n, n_cols, log_lde, cap, threads, cap_out);

@@ -76,7 +76,7 @@ def mul_stream(k, vbase, out=None):
     return I
 
 
-def reduce_stream(k, vbase):
+def reduce_stream(k, vbase, pair_out=False):
     """z = L + H * 2^32 mod p for a 64-bit pair L and H = (Hhi:Hlo) given as two 32-bit
     operands, with L < 2^63 and Hhi < 2^31 (so Hhi * EPS + L < 2^64).  These bounds hold
     for every lazily accumulated linear-layer limb in poseidon2.hpp (< 2^48).
@@ -91,8 +91,12 @@ def reduce_stream(k, vbase):
     I.append(("v_add_co_u32 %s, %s, %s, %s" % (W1, cA, W1, Hlo), set(), {cA}))
     # a carry out of the high word is 2^64 == EPS; W then < 2^48 so W + EPS cannot overflow
     I.append(("v_cndmask_b32_e64 %s, 0, -1, %s" % (M, cA), {cA}, set()))
-    I.append(("v_add_co_u32 %s, %s, %s, %s" % (z0, cA, W0, M), set(), {cA}))
-    I.append(("v_addc_co_u32 %s, %s, %s, 0, %s" % (z1, JUNK, W1, cA), {cA}, {JUNK}))
+    if pair_out:
+        # z = M * 1 + W in one 64-bit mad (z is a compiler-allocated VGPR pair)
+        I.append(("v_mad_u64_u32 %%[z%d], %s, %s, 1, %s" % (k, JUNK, M, W), set(), {JUNK}))
+    else:
+        I.append(("v_add_co_u32 %s, %s, %s, %s" % (z0, cA, W0, M), set(), {cA}))
+        I.append(("v_addc_co_u32 %s, %s, %s, 0, %s" % (z1, JUNK, W1, cA), {cA}, {JUNK}))
     return I
 
 
@@ -121,17 +125,29 @@ def addsub_stream(k, vbase, op):
     return I
 
 
-def ct_bfly_stream(k, vbase):
-    """Cooley-Tukey butterfly in place: (a, c) <- (a + c w, a - c w), 28 instructions.
+# VGPR / SGPR holding the two factors of -EPS = -65537 * 65535 (EPS = (2^16 + 1)(2^16 - 1)) for
+# the butterfly's signed-mad subtract correction; set once per asm block
+NEG_EPS_V = 0xFFFEFFFF  # -65537 as i32
+NEG_EPS_S = 0xFFFF      # 65535
+BFLY_SCONST = "s%d" % (SGPR_BASE + 26)
+
+
+def ct_bfly_stream(k, vbase, vconst):
+    """Cooley-Tukey butterfly: (A, C) <- (a + c w, a - c w), 26 instructions.
     t = c * w (mul_stream, result left in its U pair), canonicalised (t + EPS overflows iff
     t >= p).  With t < p, a - t borrows at most once and a + t wraps 2^64 at most once, so each
-    needs a single EPS correction (5 instructions instead of 8).  The difference goes into c's
-    registers (c is dead after the products), then the sum into a's.
-    Operands: a0,a1 and c0,c1 read-write; w0,w1 read."""
-    P0, P1, U0, U1 = ["v%d" % (vbase + i) for i in range(4)]
-    M = "v%d" % (vbase + 8)
-    p0, p1, p2 = sp(3 * k), sp(3 * k + 1), sp(3 * k + 2)
-    a0, a1, c0, c1 = ["%%[%s%d]" % (n, k) for n in ("a0", "a1", "c0", "c1")]
+    needs a single EPS correction, applied by one 64-bit mad into the output pair:
+      a - t = d - borrow * 2^64 == d - borrow * EPS:  C = M * 65535 + d (v_mad_i64_i32),
+          M = borrow ? -65537 : 0, since -65537 * 65535 = -EPS; no underflow (d > EPS when the
+          subtraction borrowed);
+      a + t = s + carry * 2^64 == s + carry * EPS:    A = M' * 1 + s (v_mad_u64_u32),
+          M' = carry ? EPS : 0; no overflow (s <= p - 2 when the addition carried).
+    Operands: a0,a1,c0,c1,w0,w1 read; A, C written (64-bit pairs, early clobber).
+    vconst holds -65537; BFLY_SCONST holds 65535."""
+    P0, P1, U0, U1, W0, W1, V0 = ["v%d" % (vbase + i) for i in range(7)]
+    P, W = "v[%d:%d]" % (vbase, vbase + 1), "v[%d:%d]" % (vbase + 4, vbase + 5)
+    p0, p1 = sp(3 * k), sp(3 * k + 1)
+    a0, a1, A, C = ["%%[%s%d]" % (n, k) for n in ("a0", "a1", "A", "C")]
     I = []
     for t, r, w in mul_stream(k, vbase, out=(U0, U1)):
         t = t.replace("%%[b0%d]" % k, "%%[w0%d]" % k).replace("%%[b1%d]" % k, "%%[w1%d]" % k)
@@ -142,32 +158,34 @@ def ct_bfly_stream(k, vbase):
     I.append(("v_addc_co_u32 %s, %s, %s, 0, %s" % (P1, p0, U1, p0), {p0}, {p0}))
     I.append(("v_cndmask_b32_e64 %s, %s, %s, %s" % (U0, U0, P0, p0), {p0}, set()))
     I.append(("v_cndmask_b32_e64 %s, %s, %s, %s" % (U1, U1, P1, p0), {p0}, set()))
-    # c = a - t: one borrow at most, worth -2^64 == -EPS
-    I.append(("v_sub_co_u32 %s, %s, %s, %s" % (c0, p1, a0, U0), set(), {p1}))
-    I.append(("v_subb_co_u32 %s, %s, %s, %s, %s" % (c1, p1, a1, U1, p1), {p1}, {p1}))
-    I.append(("v_cndmask_b32_e64 %s, 0, -1, %s" % (M, p1), {p1}, set()))
-    I.append(("v_sub_co_u32 %s, %s, %s, %s" % (c0, p2, c0, M), set(), {p2}))
-    I.append(("v_subb_co_u32 %s, %s, %s, 0, %s" % (c1, JUNK, c1, p2), {p2}, {JUNK}))
-    # a = a + t: one wrap at most, worth 2^64 == EPS
-    I.append(("v_add_co_u32 %s, %s, %s, %s" % (a0, p0, a0, U0), set(), {p0}))
-    I.append(("v_addc_co_u32 %s, %s, %s, %s, %s" % (a1, p0, a1, U1, p0), {p0}, {p0}))
-    I.append(("v_cndmask_b32_e64 %s, 0, -1, %s" % (M, p0), {p0}, set()))
-    I.append(("v_add_co_u32 %s, %s, %s, %s" % (a0, p1, a0, M), set(), {p1}))
-    I.append(("v_addc_co_u32 %s, %s, %s, 0, %s" % (a1, JUNK, a1, p1), {p1}, {JUNK}))
+    # C = a - t (into P), then the borrow's -EPS
+    I.append(("v_sub_co_u32 %s, %s, %s, %s" % (P0, p1, a0, U0), set(), {p1}))
+    I.append(("v_subb_co_u32 %s, %s, %s, %s, %s" % (P1, p1, a1, U1, p1), {p1}, {p1}))
+    I.append(("v_cndmask_b32_e64 %s, 0, %s, %s" % (V0, vconst, p1), {p1}, set()))
+    I.append(("v_mad_i64_i32 %s, %s, %s, %s, %s" % (C, JUNK, V0, BFLY_SCONST, P), set(), {JUNK}))
+    # A = a + t (into W), then the wrap's +EPS
+    I.append(("v_add_co_u32 %s, %s, %s, %s" % (W0, p0, a0, U0), set(), {p0}))
+    I.append(("v_addc_co_u32 %s, %s, %s, %s, %s" % (W1, p0, a1, U1, p0), {p0}, {p0}))
+    I.append(("v_cndmask_b32_e64 %s, 0, -1, %s" % (U0, p0), {p0}, set()))
+    I.append(("v_mad_u64_u32 %s, %s, %s, 1, %s" % (A, JUNK, U0, W), set(), {JUNK}))
     return I
 
 
 def emit_ct_bfly(n):
-    streams = [ct_bfly_stream(k, 10 * k) for k in range(n)]  # 64-bit tuples even-aligned
-    body = interleave(streams)
+    vconst = "v%d" % (10 * n)
+    streams = [ct_bfly_stream(k, 10 * k, vconst) for k in range(n)]  # 64-bit tuples even-aligned
+    pro = [("v_mov_b32 %s, 0x%x" % (vconst, NEG_EPS_V), set(), set()),
+           ("s_mov_b32 %s, 0x%x" % (BFLY_SCONST, NEG_EPS_S), set(), set())]
+    body = pad(pro + merge(streams))
     args, outs, ins = [], [], []
     for k in range(n):
-        args += ["uint32_t& a0%d" % k, "uint32_t& a1%d" % k, "uint32_t& c0%d" % k, "uint32_t& c1%d" % k,
-                 "uint32_t w0%d" % k, "uint32_t w1%d" % k]
-        outs += ['[%s%d] "+v"(%s%d)' % (nm, k, nm, k) for nm in ("a0", "a1", "c0", "c1")]
-        ins += ['[%s%d] "v"(%s%d)' % (nm, k, nm, k) for nm in ("w0", "w1")]
-    clob = ['"v%d"' % i for i in range(10 * n - 1)] + ['"s%d"' % i for i in range(SGPR_BASE, SGPR_BASE + 26)]
-    lines = ["// %d in-place Cooley-Tukey butterflies (a, c) <- (a + c w, a - c w) (28 instructions each)" % n,
+        args += ["uint32_t a0%d" % k, "uint32_t a1%d" % k, "uint32_t c0%d" % k, "uint32_t c1%d" % k,
+                 "uint32_t w0%d" % k, "uint32_t w1%d" % k, "uint64_t& A%d" % k, "uint64_t& C%d" % k]
+        outs += ['[%s%d] "=&v"(%s%d)' % (nm, k, nm, k) for nm in ("A", "C")]
+        ins += ['[%s%d] "v"(%s%d)' % (nm, k, nm, k) for nm in ("a0", "a1", "c0", "c1", "w0", "w1")]
+    clob = ['"v%d"' % i for i in range(10 * n + 1)] + ['"s%d"' % i for i in range(SGPR_BASE, SGPR_BASE + 27)]
+    n_v = sum(1 for t in body if t.startswith("v_"))
+    lines = ["// %d Cooley-Tukey butterflies (A, C) <- (a + c w, a - c w) (%d VALU instructions)" % (n, n_v),
              "__device__ __forceinline__ void ct_bfly_x%d(%s) {" % (n, ", ".join(args)), "    asm volatile("]
     lines += ['        "%s\\n"' % t for t in body]
     lines += ["        : %s" % ", ".join(outs), "        : %s" % ", ".join(ins), "        : %s);" % ", ".join(clob),
@@ -224,7 +242,7 @@ def pad(merged):
     return out
 
 
-def emit_fn(name, n, stream_fn, vper, in_names, out_names, in_kinds=None, doc=""):
+def emit_fn(name, n, stream_fn, vper, in_names, out_names, in_kinds=None, doc="", out_kinds=None):
     streams = [stream_fn(k, vper * k) for k in range(n)]
     body = interleave(streams)
     n_v = vper * n
@@ -234,7 +252,7 @@ def emit_fn(name, n, stream_fn, vper, in_names, out_names, in_kinds=None, doc=""
             kind = (in_kinds or {}).get(nm, "uint32_t")
             args.append("%s %s%d" % (kind, nm, k))
         for nm in out_names:
-            args.append("uint32_t& %s%d" % (nm, k))
+            args.append("%s& %s%d" % ((out_kinds or {}).get(nm, "uint32_t"), nm, k))
     outs = ", ".join('[%s%d] "=&v"(%s%d)' % (nm, k, nm, k) for k in range(n) for nm in out_names)
     ins = ", ".join('[%s%d] "v"(%s%d)' % (nm, k, nm, k) for k in range(n) for nm in in_names)
     clob = ['"v%d"' % i for i in range(n_v)] + ['"s%d"' % i for i in range(SGPR_BASE, SGPR_BASE + 26)]
@@ -255,81 +273,13 @@ def emit_fn(name, n, stream_fn, vper, in_names, out_names, in_kinds=None, doc=""
 SH = [4, 14, 11, 8, 0, 5, 2, 9, 13, 6, 3, 12]  # M_I diagonal exponents, state_generic_impl.rs:71-84
 
 
-def emit_mi_layer():
-    """Partial-round internal linear layer on a reduced state (lo[i], hi[i] 32-bit):
-    s_i' = s_i * 2^SH[i] + sum_j s_j  (M_I = diag(2^SH) + 1 1^T, state_generic_impl.rs:166-202).
-    Limb form: Ls = sum lo_j, Hs = sum hi_j (mad chains, no zero-extension), then per element
-    L = lo_i * 2^k + Ls, H = hi_i * 2^k + Hs (one mad each; < 2^47) and the 5-instruction
-    limb reduction.  One asm block, 12 elements reduced 4 at a time."""
-    SUM = {("L", c): "v[%d:%d]" % (2 * c, 2 * c + 1) for c in range(3)}
-    SUM.update({("H", c): "v[%d:%d]" % (6 + 2 * c, 7 + 2 * c) for c in range(3)})
-    consts = {}
-    sreg = SGPR_BASE + 26
-    pro = []
-    for k in sorted(set(SH)):
-        if k > 6:
-            consts[k] = "s%d" % sreg
-            pro.append(("s_mov_b32 s%d, %d" % (sreg, 1 << k), set(), set()))
-            sreg += 1
-    chains = []
-    for limb, src in (("L", "lo"), ("H", "hi")):
-        for c in range(3):
-            ch = []
-            for t in range(4):
-                i = 4 * c + t
-                acc = SUM[(limb, c)]
-                ch.append(("v_mad_u64_u32 %s, %s, %%[%s%d], 1, %s" % (acc, JUNK, src, i, "0" if t == 0 else acc),
-                           set(), {JUNK}))
-            chains.append(ch)
-    body = pro + merge(chains)
-    for limb in ("L", "H"):
-        a = SUM[(limb, 0)]
-        body.append(("v_lshl_add_u64 %s, %s, 0, %s" % (a, SUM[(limb, 1)], a), set(), set()))
-        body.append(("v_lshl_add_u64 %s, %s, 0, %s" % (a, SUM[(limb, 2)], a), set(), set()))
-    Ls, Hs = SUM[("L", 0)], SUM[("H", 0)]
-    for g in range(3):
-        streams = []
-        for j in range(4):
-            i = 4 * g + j
-            base = 12 + 8 * j
-            Lp = "v[%d:%d]" % (base, base + 1)
-            Hp = "v[%d:%d]" % (base + 2, base + 3)
-            H0, H1 = "v%d" % (base + 2), "v%d" % (base + 3)
-            Wp = "v[%d:%d]" % (base + 4, base + 5)
-            W0, W1, M = "v%d" % (base + 4), "v%d" % (base + 5), "v%d" % (base + 6)
-            K = consts.get(SH[i], str(1 << SH[i]))
-            c = sp(j)
-            st = [
-                ("v_mad_u64_u32 %s, %s, %%[lo%d], %s, %s" % (Lp, JUNK, i, K, Ls), set(), {JUNK}),
-                ("v_mad_u64_u32 %s, %s, %%[hi%d], %s, %s" % (Hp, JUNK, i, K, Hs), set(), {JUNK}),
-                ("v_mad_u64_u32 %s, %s, %s, -1, %s" % (Wp, JUNK, H1, Lp), set(), {JUNK}),
-                ("v_add_co_u32 %s, %s, %s, %s" % (W1, c, W1, H0), set(), {c}),
-                ("v_cndmask_b32_e64 %s, 0, -1, %s" % (M, c), {c}, set()),
-                ("v_add_co_u32 %%[lo%d], %s, %s, %s" % (i, c, W0, M), set(), {c}),
-                ("v_addc_co_u32 %%[hi%d], %s, %s, 0, %s" % (i, JUNK, W1, c), {c}, {JUNK}),
-            ]
-            streams.append(st)
-        body += merge(streams)
-    text = pad(body)
-    # in place: element i's result overwrites lo[i]/hi[i] only after every read of them
-    # (the sums read all inputs first; element i's own mads read lo[i]/hi[i] before its write)
-    args = ", ".join(["uint32_t* lo", "uint32_t* hi"])
-    outs = ", ".join('[lo%d] "+v"(lo[%d]), [hi%d] "+v"(hi[%d])' % (i, i, i, i) for i in range(12))
-    ins = ""
-    clob = ['"v%d"' % i for i in range(12 + 32)] + ['"s%d"' % i for i in range(SGPR_BASE, sreg)]
-    lines = ["// Poseidon2 partial-round M_I on a reduced state (%d VALU instructions)" % sum(1 for t in text if t.startswith("v_")),
-             "__device__ __forceinline__ void mi_layer(%s) {" % args, "    asm volatile("]
-    lines += ['        "%s\\n"' % t for t in text]
-    lines += ["        : %s" % outs, "        : %s" % ins, "        : %s);" % ", ".join(clob), "}"]
-    return "\n".join(lines) + "\n"
-
-
 # v_lshl_add_u64 shift amounts verified on gfx950 hardware (tools/isa_probe.hip)
 MAX_LSHL_ADD_SHIFT = 4
 
 
-def reduce_limbs(Lp, Hp, Wp, M, c, z0, z1):
-    """The 5-instruction limb reduction (reduce_stream) on register pairs Lp, Hp -> z0, z1."""
+def reduce_limbs(Lp, Hp, Wp, M, c, z):
+    """The 4-instruction limb reduction (reduce_stream, pair_out) on register pairs Lp, Hp ->
+    the 64-bit output operand z."""
     H0, H1 = Hp.split("[")[1].rstrip("]").split(":")
     H0, H1 = "v" + H0, "v" + H1
     W0, W1 = Wp.split("[")[1].rstrip("]").split(":")
@@ -338,8 +288,7 @@ def reduce_limbs(Lp, Hp, Wp, M, c, z0, z1):
         ("v_mad_u64_u32 %s, %s, %s, -1, %s" % (Wp, JUNK, H1, Lp), set(), {JUNK}),
         ("v_add_co_u32 %s, %s, %s, %s" % (W1, c, W1, H0), set(), {c}),
         ("v_cndmask_b32_e64 %s, 0, -1, %s" % (M, c), {c}, set()),
-        ("v_add_co_u32 %s, %s, %s, %s" % (z0, c, W0, M), set(), {c}),
-        ("v_addc_co_u32 %s, %s, %s, 0, %s" % (z1, JUNK, W1, c), {c}, {JUNK}),
+        ("v_mad_u64_u32 %s, %s, %s, 1, %s" % (z, JUNK, M, Wp), set(), {JUNK}),
     ]
 
 
@@ -357,7 +306,8 @@ def _consts(pro):
 def emit_mi_layer_a():
     """First partial round of a pair: M_I with elements 1..11 left as unreduced limbs.
     L_i = lo_i 2^SH[i] + sum lo_j, H_i likewise (one mad each, < 2^46.6); only element 0,
-    the next S-box input, is reduced.  The pair's second round (mi_layer_b) reduces all."""
+    the next S-box input, is reduced (into the 64-bit z0).  The pair's second round
+    (mi_layer_b) reduces all."""
     pro = []
     consts, sreg = _consts(pro)
     SUM = {("L", c): "v[%d:%d]" % (2 * c, 2 * c + 1) for c in range(3)}
@@ -384,12 +334,12 @@ def emit_mi_layer_a():
         body.append(("v_mad_u64_u32 %%[H%d], %s, %%[hi%d], %s, %s" % (i, JUNK, i, K, Hs), set(), {JUNK}))
     body.append(("v_mad_u64_u32 v[12:13], %s, %%[lo0], %d, %s" % (JUNK, 1 << SH[0], Ls), set(), {JUNK}))
     body.append(("v_mad_u64_u32 v[14:15], %s, %%[hi0], %d, %s" % (JUNK, 1 << SH[0], Hs), set(), {JUNK}))
-    body += reduce_limbs("v[12:13]", "v[14:15]", "v[16:17]", "v18", sp(0), "%[lo0]", "%[hi0]")
+    body += reduce_limbs("v[12:13]", "v[14:15]", "v[16:17]", "v18", sp(0), "%[z0]")
     text = pad(body)
-    args = "uint32_t* lo, uint32_t* hi, uint64_t* L, uint64_t* H"
-    outs = ['[lo0] "+v"(lo[0])', '[hi0] "+v"(hi[0])']
+    args = "const uint32_t* lo, const uint32_t* hi, uint64_t* L, uint64_t* H, uint64_t& z0"
+    outs = ['[z0] "=&v"(z0)']
     outs += ['[L%d] "=&v"(L[%d]), [H%d] "=&v"(H[%d])' % (i, i, i, i) for i in range(1, 12)]
-    ins = ['[lo%d] "v"(lo[%d]), [hi%d] "v"(hi[%d])' % (i, i, i, i) for i in range(1, 12)]
+    ins = ['[lo%d] "v"(lo[%d]), [hi%d] "v"(hi[%d])' % (i, i, i, i) for i in range(12)]
     clob = ['"v%d"' % i for i in range(20)] + ['"s%d"' % i for i in range(SGPR_BASE, sreg)]
     n_v = sum(1 for t in text if t.startswith("v_"))
     lines = ["// Poseidon2 partial round M_I, first of a pair: elements 1..11 as limbs L, H (%d VALU instructions)" % n_v,
@@ -403,7 +353,7 @@ def emit_mi_layer_b():
     """Second partial round of a pair: M_I on element 0 (reduced lo0, hi0) and elements 1..11
     as the limbs L_i, H_i < 2^46.6 left by mi_layer_a.  Sums over limbs < 2^50.2;
     L_i' = L_i << SH[i] + sum < 2^61 (one v_lshl_add_u64 when SH[i] <= MAX_LSHL_ADD_SHIFT,
-    else shift + add); then the 5-instruction reduction of every element."""
+    else shift + add); then the 4-instruction reduction of every element into the 64-bit z[i]."""
     pro = []
     consts, sreg = _consts(pro)
     Ls, Hs = "v[0:1]", "v[2:3]"
@@ -443,14 +393,14 @@ def emit_mi_layer_b():
                     else:
                         st.append(("v_lshlrev_b64 %s, %d, %%[%s%d]" % (P, SH[i], lim, i), set(), set()))
                         st.append(("v_lshl_add_u64 %s, %s, 0, %s" % (P, P, S), set(), set()))
-            st += reduce_limbs(Lp, Hp, Wp, M, c, "%%[lo%d]" % i, "%%[hi%d]" % i)
+            st += reduce_limbs(Lp, Hp, Wp, M, c, "%%[z%d]" % i)
             streams.append(st)
         body += merge(streams)
     text = pad(body)
-    args = "uint32_t* lo, uint32_t* hi, const uint64_t* L, const uint64_t* H"
-    outs = ['[lo0] "+v"(lo[0])', '[hi0] "+v"(hi[0])']
-    outs += ['[lo%d] "=&v"(lo[%d]), [hi%d] "=&v"(hi[%d])' % (i, i, i, i) for i in range(1, 12)]
-    ins = ['[L%d] "v"(L[%d]), [H%d] "v"(H[%d])' % (i, i, i, i) for i in range(1, 12)]
+    args = "uint32_t lo0, uint32_t hi0, const uint64_t* L, const uint64_t* H, uint64_t* z"
+    outs = ['[z%d] "=&v"(z[%d])' % (i, i) for i in range(12)]
+    ins = ['[lo0] "v"(lo0)', '[hi0] "v"(hi0)']
+    ins += ['[L%d] "v"(L[%d]), [H%d] "v"(H[%d])' % (i, i, i, i) for i in range(1, 12)]
     clob = ['"v%d"' % i for i in range(8 + 32)] + ['"s%d"' % i for i in range(SGPR_BASE, sreg)]
     n_v = sum(1 for t in text if t.startswith("v_"))
     lines = ["// Poseidon2 partial round M_I, second of a pair: reduces every element (%d VALU instructions)" % n_v,
@@ -474,9 +424,10 @@ namespace glasm {
         parts.append(emit_fn("mul_x%d" % n, n, mul_stream, 10, ["a0", "a1", "b0", "b1"], ["z0", "z1"],
                              doc="%d independent products z = a * b mod p (14 instructions each)" % n))
     for n in (1, 2, 3, 4):
-        parts.append(emit_fn("reduce_x%d" % n, n, reduce_stream, 4, ["L", "Hlo", "Hhi"], ["z0", "z1"],
-                             in_kinds={"L": "uint64_t"},
-                             doc="%d reductions z = L + (Hhi:Hlo) * 2^32 mod p, L and H < 2^63" % n))
+        parts.append(emit_fn("reduce_x%d" % n, n, lambda k, vb: reduce_stream(k, vb, pair_out=True), 4,
+                             ["L", "Hlo", "Hhi"], ["z"], in_kinds={"L": "uint64_t"}, out_kinds={"z": "uint64_t"},
+                             doc="%d reductions z = L + (Hhi:Hlo) * 2^32 mod p, L and H < 2^63 "
+                                 "(4 instructions each, z a 64-bit register pair)" % n))
     for n in (1, 2, 4):
         parts.append(emit_fn("add_x%d" % n, n, lambda k, vb: addsub_stream(k, vb, "add"), 2,
                              ["a0", "a1", "b0", "b1"], ["z0", "z1"], doc="%d general additions" % n))
@@ -487,7 +438,6 @@ namespace glasm {
     for n in (1, 2, 4):
         parts.append(emit_fn("canon_x%d" % n, n, canon_stream, 2, ["a0", "a1"], ["z0", "z1"],
                              doc="%d canonicalisations z = x mod p in [0, p)" % n))
-    parts.append(emit_mi_layer())
     parts.append(emit_mi_layer_a())
     parts.append(emit_mi_layer_b())
     parts.append("}  // namespace glasm\n")
