@@ -401,3 +401,105 @@ def sharded_query(ws, tree_idx):
     buf = buf.cpu()
     c = ws.n_cols
     return buf[:c], buf[c:c + 4], buf[c + 4:].reshape(-1, 4)
+
+
+# ------------------------------------------------------------------ native collective commit
+HASHER_IDS = {"poseidon2": 0, "blake2s": 1, "keccak256": 2}
+
+
+def native_columns(n_cols, world, rank, hasher="poseidon2"):
+    """bj_sharded_columns: the global trace columns rank `rank` of `world` holds, in the order of
+    its trace-shard rows (the same deal as ShardedWorkspace.my_columns, except that at G = 1 the
+    native commit runs one chunk).  Host logic only."""
+    import ctypes
+    from ._lib import load, check
+    log_g = _log2(world)
+    out = (ctypes.c_uint32 * (n_cols // world if n_cols % world == 0 and n_cols else 1))()
+    check(load().bj_sharded_columns(n_cols, log_g, rank, HASHER_IDS[hasher], out), "bj_sharded_columns")
+    return list(out)
+
+
+class LocalGroup:
+    """bj_comm_local_group_*: in-process ranks (threads) sharing one device.  A rehearsal
+    transport that runs the native pipeline multi-rank on one GPU; not for performance."""
+
+    def __init__(self, world):
+        import ctypes
+        from ._lib import load, check
+        h = ctypes.c_void_p()
+        check(load().bj_comm_local_group_create(world, ctypes.byref(h)), "bj_comm_local_group_create")
+        self.handle, self.world = h, world
+
+    def comm(self, rank):
+        return NativeComm._make("bj_comm_init_local", self.handle, rank, world=self.world, rank=rank, keep=self)
+
+    def close(self):
+        from ._lib import load
+        if self.handle:
+            load().bj_comm_local_group_destroy(self.handle)
+            self.handle = None
+
+
+class NativeComm:
+    """An opaque bj_comm (include/boojum_mi355x.h): the communicator of bj_sharded_commit_d."""
+
+    def __init__(self, handle, world, rank, keep=None):
+        self.handle, self.world, self.rank, self._keep = handle, world, rank, keep
+
+    @classmethod
+    def _make(cls, fn, *args, world, rank, keep=None):
+        import ctypes
+        from ._lib import load, check
+        h = ctypes.c_void_p()
+        check(getattr(load(), fn)(*args, ctypes.byref(h)), fn)
+        return cls(h, world, rank, keep)
+
+    @classmethod
+    def rccl(cls, group=None):
+        """A fresh RCCL communicator over the ranks of the torch.distributed group (one process
+        per GPU, current device): rank 0 makes the unique id, the group broadcasts it, every rank
+        joins (ncclCommInitRank).  Collective."""
+        import ctypes
+        import torch.distributed as dist
+        from ._lib import load, check
+        world, rank = dist.get_world_size(group), dist.get_rank(group)
+        uid = (ctypes.c_uint8 * 128)()
+        if rank == 0:
+            check(load().bj_comm_rccl_unique_id(uid), "bj_comm_rccl_unique_id")
+        box = [bytes(uid)]
+        dist.broadcast_object_list(box, src=dist.get_global_rank(group, 0) if group is not None else 0, group=group)
+        uid = (ctypes.c_uint8 * 128).from_buffer_copy(box[0])
+        return cls._make("bj_comm_init_rccl", uid, world, rank, world=world, rank=rank)
+
+    def close(self):
+        from ._lib import load
+        if self.handle:
+            load().bj_comm_destroy(self.handle)
+            self.handle = None
+
+
+class NativeShardedResult:
+    """Rank P's outputs of bj_sharded_commit_d: lde (C, m), leaves (m, 4), nodes
+    (m - cap_local, 4), cap (cap, 4), all int64 on the device."""
+
+    def __init__(self, n_cols, log_n, log_lde, cap_size, world, device="cuda"):
+        m = ((1 << log_n) << log_lde) // world
+        cap_local = max(1, cap_size // world)
+        kw = dict(dtype=torch.int64, device=device)
+        self.m, self.cap_local = m, cap_local
+        self.lde = torch.empty((n_cols, m), **kw)
+        self.leaves = torch.empty((m, 4), **kw)
+        self.nodes = torch.empty((m - cap_local, 4), **kw)
+        self.cap = torch.empty((cap_size, 4), **kw)
+
+
+def native_sharded_commit(comm, trace_shard, n_cols, log_n, log_lde, cap_size, hasher="poseidon2", out=None):
+    """bj_sharded_commit_d on the current stream: this rank's part of the G-way witness commit,
+    trace_shard (C/G, n) in native_columns order.  Collective over `comm`."""
+    if tuple(trace_shard.shape) != (n_cols // comm.world, 1 << log_n) or trace_shard.stride(1) != 1:
+        raise ValueError("trace shard must be (%d, %d) with unit-stride rows" % (n_cols // comm.world, 1 << log_n))
+    out = out or NativeShardedResult(n_cols, log_n, log_lde, cap_size, comm.world, trace_shard.device)
+    call("bj_sharded_commit_d", comm.handle, trace_shard.data_ptr(), trace_shard.stride(0), n_cols, log_n, log_lde,
+         cap_size, HASHER_IDS[hasher], out.lde.data_ptr(), out.leaves.data_ptr(), out.nodes.data_ptr(),
+         out.cap.data_ptr(), stream_of(out.lde))
+    return out

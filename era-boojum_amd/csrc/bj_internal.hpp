@@ -90,3 +90,8 @@ hipError_t launch_fri_fold(const uint64_t* c0, const uint64_t* c1, size_t n_out,
                            uint64_t coset_inverse, uint64_t ch0, uint64_t ch1, uint64_t* d0, uint64_t* d1,
                            hipStream_t st);
 }  // namespace bj
+
+namespace bj {
+// capi.hip: set the calling thread's bj_last_error() message; returns code
+int set_error(int code, const char* msg);
+}  // namespace bj

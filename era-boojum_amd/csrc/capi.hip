@@ -351,6 +351,10 @@ int shard_from_folded(const uint64_t* folded, size_t folded_stride, uint32_t n_c
 }
 }  // namespace
 
+namespace bj {
+int set_error(int code, const char* msg) { return fail(code, msg); }
+}  // namespace bj
+
 extern "C" {
 
 const char* bj_last_error(void) { return g_err.c_str(); }

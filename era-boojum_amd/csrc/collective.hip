@@ -1,0 +1,518 @@
+// Collective sharded witness commit: the multi-GPU split of the commitment as one native call
+// per rank (include/boojum_mi355x.h, "collective sharded commit").
+//
+// The reference commits on one host (transform_raw_storages_to_lde, utils.rs:270-403, then
+// MerkleTreeWithCap::construct, merkle_tree.rs:78-172, driven by prover.rs:313-353).  Here the
+// flat leaf domain (coset * n + row) is cut into G contiguous ranges, one per rank, and every
+// rank hashes a subtree of the reference's tree.  The only data exchange is per column chunk:
+//   G <= D  all-gather of the chunk's coefficients (bj_lde_coeffs_d format), then this rank's
+//           whole cosets (bj_lde_shard_d);
+//   G >  D  the sender folds its own columns for every rank (bj_lde_fold_shards_d), one
+//           all-to-all delivers them, then this rank's sub-coset (bj_lde_shard_folded_d).
+// Chunk k's exchange runs on a high-priority stream while the compute stream transforms and
+// absorbs the chunks that have already arrived; the leaf sponge carries its capacity words
+// (Poseidon2) or chaining value (Blake2s) between chunks.  The cap is all-gathered at the end.
+//
+// Transports behind bj_comm: RCCL (resolved with dlopen, so the library loads without it) and
+// an in-process "local" group of ranks sharing one device (device-to-device copies ordered by
+// events through a host barrier), which runs the same pipeline multi-rank on a single GPU.
+#include <hip/hip_runtime.h>
+#include <rccl/rccl.h>
+#include <dlfcn.h>
+
+#include <algorithm>
+#include <condition_variable>
+#include <cstring>
+#include <mutex>
+#include <string>
+#include <vector>
+
+#include "../../include/boojum_mi355x.h"
+#include "bj_internal.hpp"
+
+namespace {
+
+int err(int code, const std::string& msg) { return bj::set_error(code, msg.c_str()); }
+
+#define HIP_CHECK(expr, what)                                                            \
+    do {                                                                                 \
+        hipError_t e_ = (expr);                                                          \
+        if (e_ != hipSuccess) return err(BJ_EHIP, std::string(what) + ": " + hipGetErrorString(e_)); \
+    } while (0)
+
+#define BJ_CHECK(expr)               \
+    do {                             \
+        if (int r_ = (expr)) return r_; \
+    } while (0)
+
+// ------------------------------------------------------------------ RCCL, at run time
+struct Rccl {
+    decltype(&ncclGetUniqueId) get_unique_id = nullptr;
+    decltype(&ncclCommInitRank) init_rank = nullptr;
+    decltype(&ncclCommDestroy) destroy = nullptr;
+    decltype(&ncclAllGather) all_gather = nullptr;
+    decltype(&ncclSend) send = nullptr;
+    decltype(&ncclRecv) recv = nullptr;
+    decltype(&ncclGroupStart) group_start = nullptr;
+    decltype(&ncclGroupEnd) group_end = nullptr;
+    decltype(&ncclGetErrorString) error_string = nullptr;
+    bool ok = false;
+    std::string why;
+};
+
+// The process's RCCL: the copy already loaded (torch's, say) when there is one, so a
+// communicator made by the caller and our calls on it use the same library.
+const Rccl& rccl() {
+    static Rccl r;
+    static std::once_flag once;
+    std::call_once(once, [] {
+        void* h = dlopen("librccl.so.1", RTLD_NOW | RTLD_NOLOAD);
+        if (!h) h = dlopen("librccl.so.1", RTLD_NOW);
+        if (!h) {
+            const char* e = dlerror();
+            r.why = std::string("cannot load librccl.so.1: ") + (e ? e : "");
+            return;
+        }
+#define RCCL_SYM(field, name)                                             \
+    r.field = reinterpret_cast<decltype(r.field)>(dlsym(h, name));       \
+    if (!r.field) {                                                       \
+        r.why = "librccl.so.1 does not export " name;                     \
+        return;                                                           \
+    }
+        RCCL_SYM(get_unique_id, "ncclGetUniqueId")
+        RCCL_SYM(init_rank, "ncclCommInitRank")
+        RCCL_SYM(destroy, "ncclCommDestroy")
+        RCCL_SYM(all_gather, "ncclAllGather")
+        RCCL_SYM(send, "ncclSend")
+        RCCL_SYM(recv, "ncclRecv")
+        RCCL_SYM(group_start, "ncclGroupStart")
+        RCCL_SYM(group_end, "ncclGroupEnd")
+        RCCL_SYM(error_string, "ncclGetErrorString")
+#undef RCCL_SYM
+        r.ok = true;
+    });
+    return r;
+}
+
+int rccl_fail(const Rccl& r, ncclResult_t e, const char* what) {
+    return err(BJ_EHIP, std::string(what) + ": " + r.error_string(e));
+}
+
+#define RCCL_CHECK(R, expr, what)                                   \
+    do {                                                            \
+        ncclResult_t e_ = (expr);                                   \
+        if (e_ != ncclSuccess) return rccl_fail(R, e_, what);       \
+    } while (0)
+
+// ----------------------------------------------------- in-process rank group (one device)
+struct LocalGroup {
+    int world = 0;
+    std::mutex mu;
+    std::condition_variable cv;
+    int arrived = 0;
+    uint64_t generation = 0;
+    std::vector<const void*> slot;
+    std::vector<hipEvent_t> ready, done;
+
+    void barrier() {
+        std::unique_lock<std::mutex> lk(mu);
+        const uint64_t g = generation;
+        if (++arrived == world) {
+            arrived = 0;
+            generation++;
+            cv.notify_all();
+        } else {
+            cv.wait(lk, [&] { return generation != g; });
+        }
+    }
+};
+
+}  // namespace
+
+struct bj_comm {
+    enum Kind { RCCL_OWNED, RCCL_WRAPPED, LOCAL } kind;
+    int world = 1, rank = 0;
+    ncclComm_t nccl = nullptr;
+    LocalGroup* group = nullptr;
+    hipStream_t xs = nullptr;  // exchange stream, high priority, created on first use
+    int xs_dev = -1;
+};
+
+namespace {
+
+int exchange_stream(bj_comm* c, hipStream_t* out) {
+    int dev = 0;
+    HIP_CHECK(hipGetDevice(&dev), "hipGetDevice");
+    if (c->xs && c->xs_dev != dev) return err(BJ_EINVAL, "communicator used from another device");
+    if (!c->xs) {
+        int least = 0, greatest = 0;
+        HIP_CHECK(hipDeviceGetStreamPriorityRange(&least, &greatest), "stream priority range");
+        HIP_CHECK(hipStreamCreateWithPriority(&c->xs, hipStreamNonBlocking, greatest), "hipStreamCreate");
+        c->xs_dev = dev;
+    }
+    *out = c->xs;
+    return BJ_OK;
+}
+
+// recv block p <- rank p's send block (all-to-all: its block `rank`; all-gather: its only one)
+int local_exchange(bj_comm* c, const void* send, void* recv, size_t bytes, bool all_to_all, hipStream_t st) {
+    LocalGroup& g = *c->group;
+    const int me = c->rank;
+    HIP_CHECK(hipEventRecord(g.ready[me], st), "hipEventRecord");
+    g.slot[me] = send;
+    g.barrier();  // every rank's send buffer and ready event are published
+    for (int p = 0; p < g.world; p++) {
+        HIP_CHECK(hipStreamWaitEvent(st, g.ready[p], 0), "hipStreamWaitEvent");
+        const char* src = static_cast<const char*>(g.slot[p]) + (all_to_all ? (size_t)me * bytes : 0);
+        char* dst = static_cast<char*>(recv) + (size_t)p * bytes;
+        if (src != dst && bytes) HIP_CHECK(hipMemcpyAsync(dst, src, bytes, hipMemcpyDeviceToDevice, st), "memcpy");
+    }
+    HIP_CHECK(hipEventRecord(g.done[me], st), "hipEventRecord");
+    g.barrier();  // every rank has queued its reads of the others' buffers
+    for (int p = 0; p < g.world; p++) HIP_CHECK(hipStreamWaitEvent(st, g.done[p], 0), "hipStreamWaitEvent");
+    g.barrier();  // nobody re-records this round's events before all waits are queued
+    return BJ_OK;
+}
+
+// recv (world x bytes) <- concat over ranks of send (bytes); send may be recv + rank * bytes
+int all_gather(bj_comm* c, const void* send, void* recv, size_t bytes, hipStream_t st) {
+    if (c->world == 1) {
+        if (send != recv && bytes) HIP_CHECK(hipMemcpyAsync(recv, send, bytes, hipMemcpyDeviceToDevice, st), "memcpy");
+        return BJ_OK;
+    }
+    if (c->kind == bj_comm::LOCAL) return local_exchange(c, send, recv, bytes, false, st);
+    const Rccl& R = rccl();
+    RCCL_CHECK(R, R.all_gather(send, recv, bytes / 8, ncclUint64, c->nccl, st), "ncclAllGather");
+    return BJ_OK;
+}
+
+// recv block p (bytes) <- block `rank` of rank p's send (world x bytes)
+int all_to_all(bj_comm* c, const void* send, void* recv, size_t bytes, hipStream_t st) {
+    if (c->world == 1) {
+        if (send != recv && bytes) HIP_CHECK(hipMemcpyAsync(recv, send, bytes, hipMemcpyDeviceToDevice, st), "memcpy");
+        return BJ_OK;
+    }
+    if (c->kind == bj_comm::LOCAL) return local_exchange(c, send, recv, bytes, true, st);
+    const Rccl& R = rccl();
+    RCCL_CHECK(R, R.group_start(), "ncclGroupStart");
+    for (int p = 0; p < c->world; p++) {
+        const char* s = static_cast<const char*>(send) + (size_t)p * bytes;
+        char* d = static_cast<char*>(recv) + (size_t)p * bytes;
+        RCCL_CHECK(R, R.send(s, bytes / 8, ncclUint64, p, c->nccl, st), "ncclSend");
+        RCCL_CHECK(R, R.recv(d, bytes / 8, ncclUint64, p, c->nccl, st), "ncclRecv");
+    }
+    RCCL_CHECK(R, R.group_end(), "ncclGroupEnd");
+    return BJ_OK;
+}
+
+// ------------------------------------------------------------------ column pipeline plan
+bool is_pow2(uint64_t x) { return x && !(x & (x - 1)); }
+
+uint32_t log2u(uint64_t x) {
+    uint32_t l = 0;
+    while ((1ull << l) < x) l++;
+    return l;
+}
+
+struct Run {
+    uint32_t lo, global, count;  // local first row, global first column, columns
+    uint32_t c0, c1;             // the chunk's global column range
+};
+
+// The column deal of sharded.py (_chunk_unit, _chunk_schedule, column_runs): chunk k is
+// G * c_k consecutive columns, c = u, u, 2u, 4u, ... capped at 32 rounded to u, u = 8/gcd(8, G);
+// rank P holds the P-th run of c_k.  One chunk (contiguous ownership) when C/G is not a
+// multiple of u, for a hasher without column continuation, or at G = 1 (nothing to overlap).
+std::vector<Run> column_runs(uint32_t n_cols, uint32_t world, uint32_t rank, int hasher) {
+    const uint32_t cpr = n_cols / world;
+    uint32_t gcd = 8, w = world;
+    while (w) {
+        uint32_t t = gcd % w;
+        gcd = w;
+        w = t;
+    }
+    const uint32_t unit = 8 / gcd;
+    const bool partial = hasher == BJ_HASHER_POSEIDON2 || hasher == BJ_HASHER_BLAKE2S;
+    std::vector<Run> runs;
+    if (world == 1 || cpr % unit != 0 || !partial) {
+        runs.push_back({0, rank * cpr, cpr, 0, n_cols});
+        return runs;
+    }
+    const uint32_t max_cols = std::max(unit, 32 / unit * unit);
+    uint32_t done = 0, b = unit;
+    while (done < cpr) {
+        const uint32_t take = std::min(b, cpr - done);
+        runs.push_back({done, done * world + rank * take, take, done * world, (done + take) * world});
+        done += take;
+        if (runs.size() >= 2) b = std::min(2 * b, max_cols);
+    }
+    return runs;
+}
+
+// Stream-ordered workspace, freed on the stream at scope exit.
+struct Workspace {
+    hipStream_t st;
+    std::vector<void*> ptrs;
+    explicit Workspace(hipStream_t s) : st(s) {}
+    hipError_t alloc(uint64_t** p, size_t elems) {
+        hipError_t e = hipMallocAsync(reinterpret_cast<void**>(p), std::max<size_t>(elems, 1) * 8, st);
+        if (e == hipSuccess) ptrs.push_back(*p);
+        return e;
+    }
+    ~Workspace() {
+        for (void* p : ptrs) (void)hipFreeAsync(p, st);
+    }
+};
+
+struct Events {
+    std::vector<hipEvent_t> ev;
+    hipError_t make(size_t n) {
+        for (size_t i = 0; i < n; i++) {
+            hipEvent_t e;
+            hipError_t r = hipEventCreateWithFlags(&e, hipEventDisableTiming);
+            if (r != hipSuccess) return r;
+            ev.push_back(e);
+        }
+        return hipSuccess;
+    }
+    ~Events() {
+        for (hipEvent_t e : ev) (void)hipEventDestroy(e);
+    }
+};
+
+int nodes_for(int hasher, const uint64_t* leaves, size_t n, uint32_t cap, uint64_t* nodes, void* st) {
+    switch (hasher) {
+        case BJ_HASHER_POSEIDON2: return bj_merkle_nodes_d(leaves, n, cap, nodes, st);
+        case BJ_HASHER_BLAKE2S: return bj_blake2s_nodes_d(leaves, n, cap, nodes, st);
+        default: return bj_keccak256_nodes_d(leaves, n, cap, nodes, st);
+    }
+}
+
+}  // namespace
+
+extern "C" {
+
+int bj_comm_rccl_unique_id(uint8_t* id_out128) {
+    if (!id_out128) return err(BJ_EINVAL, "null id buffer");
+    const Rccl& R = rccl();
+    if (!R.ok) return err(BJ_EHIP, R.why);
+    ncclUniqueId id;
+    RCCL_CHECK(R, R.get_unique_id(&id), "ncclGetUniqueId");
+    static_assert(sizeof(id) == 128, "ncclUniqueId is 128 bytes");
+    std::memcpy(id_out128, &id, sizeof(id));
+    return BJ_OK;
+}
+
+int bj_comm_init_rccl(const uint8_t* id128, int world, int rank, bj_comm** out) {
+    if (!id128 || !out) return err(BJ_EINVAL, "null argument");
+    if (world < 1 || !is_pow2((uint64_t)world) || rank < 0 || rank >= world)
+        return err(BJ_EINVAL, "world must be a power of two and 0 <= rank < world");
+    const Rccl& R = rccl();
+    if (!R.ok) return err(BJ_EHIP, R.why);
+    ncclUniqueId id;
+    std::memcpy(&id, id128, sizeof(id));
+    ncclComm_t comm = nullptr;
+    RCCL_CHECK(R, R.init_rank(&comm, world, id, rank), "ncclCommInitRank");
+    bj_comm* c = new bj_comm();
+    c->kind = bj_comm::RCCL_OWNED;
+    c->world = world;
+    c->rank = rank;
+    c->nccl = comm;
+    *out = c;
+    return BJ_OK;
+}
+
+int bj_comm_wrap_rccl(void* nccl_comm, int world, int rank, bj_comm** out) {
+    if (!nccl_comm || !out) return err(BJ_EINVAL, "null argument");
+    if (world < 1 || !is_pow2((uint64_t)world) || rank < 0 || rank >= world)
+        return err(BJ_EINVAL, "world must be a power of two and 0 <= rank < world");
+    const Rccl& R = rccl();
+    if (!R.ok) return err(BJ_EHIP, R.why);
+    bj_comm* c = new bj_comm();
+    c->kind = bj_comm::RCCL_WRAPPED;
+    c->world = world;
+    c->rank = rank;
+    c->nccl = static_cast<ncclComm_t>(nccl_comm);
+    *out = c;
+    return BJ_OK;
+}
+
+int bj_comm_local_group_create(int world, void** group_out) {
+    if (!group_out) return err(BJ_EINVAL, "null argument");
+    if (world < 1 || !is_pow2((uint64_t)world) || world > 64) return err(BJ_EINVAL, "world must be a power of two <= 64");
+    LocalGroup* g = new LocalGroup();
+    g->world = world;
+    g->slot.assign(world, nullptr);
+    for (int i = 0; i < 2 * world; i++) {
+        hipEvent_t e;
+        hipError_t r = hipEventCreateWithFlags(&e, hipEventDisableTiming);
+        if (r != hipSuccess) {
+            for (hipEvent_t x : g->ready) (void)hipEventDestroy(x);
+            for (hipEvent_t x : g->done) (void)hipEventDestroy(x);
+            delete g;
+            return err(BJ_EHIP, std::string("hipEventCreate: ") + hipGetErrorString(r));
+        }
+        (i < world ? g->ready : g->done).push_back(e);
+    }
+    *group_out = g;
+    return BJ_OK;
+}
+
+int bj_comm_local_group_destroy(void* group) {
+    LocalGroup* g = static_cast<LocalGroup*>(group);
+    if (!g) return BJ_OK;
+    for (hipEvent_t e : g->ready) (void)hipEventDestroy(e);
+    for (hipEvent_t e : g->done) (void)hipEventDestroy(e);
+    delete g;
+    return BJ_OK;
+}
+
+int bj_comm_init_local(void* group, int rank, bj_comm** out) {
+    LocalGroup* g = static_cast<LocalGroup*>(group);
+    if (!g || !out) return err(BJ_EINVAL, "null argument");
+    if (rank < 0 || rank >= g->world) return err(BJ_EINVAL, "rank out of range");
+    bj_comm* c = new bj_comm();
+    c->kind = bj_comm::LOCAL;
+    c->world = g->world;
+    c->rank = rank;
+    c->group = g;
+    *out = c;
+    return BJ_OK;
+}
+
+int bj_comm_destroy(bj_comm* c) {
+    if (!c) return BJ_OK;
+    int rc = BJ_OK;
+    if (c->xs) (void)hipStreamDestroy(c->xs);
+    if (c->kind == bj_comm::RCCL_OWNED && c->nccl) {
+        const Rccl& R = rccl();
+        ncclResult_t e = R.destroy(c->nccl);
+        if (e != ncclSuccess) rc = rccl_fail(R, e, "ncclCommDestroy");
+    }
+    delete c;
+    return rc;
+}
+
+int bj_sharded_columns(uint32_t n_cols, uint32_t log_shards, uint32_t shard, int hasher, uint32_t* cols_out) {
+    if (log_shards > 16) return err(BJ_EINVAL, "too many shards");
+    const uint32_t world = 1u << log_shards;
+    if (!cols_out || shard >= world || n_cols % world)
+        return err(BJ_EINVAL, "need n_cols a multiple of the shard count and shard < G");
+    if (hasher < BJ_HASHER_POSEIDON2 || hasher > BJ_HASHER_KECCAK256) return err(BJ_EINVAL, "unknown hasher");
+    size_t j = 0;
+    for (const Run& r : column_runs(n_cols, world, shard, hasher))
+        for (uint32_t i = 0; i < r.count; i++) cols_out[j++] = r.global + i;
+    return BJ_OK;
+}
+
+int bj_sharded_commit_d(bj_comm* comm, const uint64_t* trace_shard, size_t trace_stride, uint32_t n_cols,
+                        uint32_t log_n, uint32_t log_lde, uint32_t cap_size, int hasher, uint64_t* lde,
+                        uint64_t* leaves, uint64_t* nodes, uint64_t* cap, void* stream) {
+    if (!comm) return err(BJ_EINVAL, "null communicator");
+    if (hasher < BJ_HASHER_POSEIDON2 || hasher > BJ_HASHER_KECCAK256) return err(BJ_EINVAL, "unknown hasher");
+    const uint32_t world = (uint32_t)comm->world, rank = (uint32_t)comm->rank;
+    const uint32_t log_g = log2u(world);
+    if (n_cols == 0 || n_cols % world) return err(BJ_EINVAL, "n_cols must be a positive multiple of the world size");
+    if (log_lde == 0) return err(BJ_EINVAL, "lde degree must be > 1 (utils.rs:283)");
+    if (log_n > 30 || log_g > log_n + log_lde) return err(BJ_EINVAL, "more shards than leaves");
+    const size_t n = (size_t)1 << log_n, nl = n << log_lde, m = nl >> log_g;
+    if (!is_pow2(cap_size) || nl <= cap_size)
+        return err(BJ_EINVAL, "need power-of-two cap_size < n * D (merkle_tree.rs:83-96)");
+    const uint32_t cap_local = std::max<uint32_t>(1, cap_size / world);
+    if (m <= cap_local) return err(BJ_EINVAL, "each shard needs more leaves than its cap slice");
+    if (trace_stride < n) return err(BJ_EINVAL, "trace_stride < n");
+    if (!trace_shard || !lde || !leaves || !nodes || !cap) return err(BJ_EINVAL, "null buffer");
+
+    hipStream_t st = reinterpret_cast<hipStream_t>(stream);
+    hipStream_t xs = nullptr;
+    if (world > 1) BJ_CHECK(exchange_stream(comm, &xs));
+    const uint32_t cpr = n_cols / world;
+    const bool fold = log_g > log_lde;
+    const std::vector<Run> runs = column_runs(n_cols, world, rank, hasher);
+    const size_t K = runs.size();
+
+    Workspace ws(st);
+    uint64_t *coeffs = nullptr, *own = nullptr, *send = nullptr, *folded = nullptr, *state = nullptr;
+    if (fold) {
+        HIP_CHECK(ws.alloc(&own, (size_t)cpr * n), "hipMallocAsync");
+        HIP_CHECK(ws.alloc(&send, (size_t)cpr * world * m), "hipMallocAsync");
+        HIP_CHECK(ws.alloc(&folded, (size_t)n_cols * m), "hipMallocAsync");
+    } else {
+        HIP_CHECK(ws.alloc(&coeffs, (size_t)n_cols * n), "hipMallocAsync");
+    }
+    if (K > 1) HIP_CHECK(ws.alloc(&state, m * 4), "hipMallocAsync");
+    Events in, arrived;
+    if (world > 1) {
+        HIP_CHECK(in.make(K), "hipEventCreate");
+        HIP_CHECK(arrived.make(K), "hipEventCreate");
+    }
+
+    // 1. local inverse transforms (and folds), each chunk's exchange issued as soon as its
+    //    part is ready
+    for (size_t k = 0; k < K; k++) {
+        const Run& r = runs[k];
+        const uint64_t* tr = trace_shard + (size_t)r.lo * trace_stride;
+        if (fold) {
+            uint64_t* snd = send + (size_t)world * m * r.lo;
+            BJ_CHECK(bj_lde_coeffs_d(tr, r.count, trace_stride, log_n, own + (size_t)r.lo * n, n, st));
+            BJ_CHECK(bj_lde_fold_shards_d(own + (size_t)r.lo * n, r.count, n, log_n, log_lde, log_g, snd,
+                                          (size_t)r.count * m, st));
+            if (world > 1) {
+                HIP_CHECK(hipEventRecord(in.ev[k], st), "hipEventRecord");
+                HIP_CHECK(hipStreamWaitEvent(xs, in.ev[k], 0), "hipStreamWaitEvent");
+                BJ_CHECK(all_to_all(comm, snd, folded + (size_t)r.c0 * m, (size_t)r.count * m * 8, xs));
+                HIP_CHECK(hipEventRecord(arrived.ev[k], xs), "hipEventRecord");
+            } else {
+                BJ_CHECK(all_to_all(comm, snd, folded + (size_t)r.c0 * m, (size_t)r.count * m * 8, st));
+            }
+        } else {
+            uint64_t* mine = coeffs + (size_t)r.global * n;
+            BJ_CHECK(bj_lde_coeffs_d(tr, r.count, trace_stride, log_n, mine, n, st));
+            if (world > 1) {
+                HIP_CHECK(hipEventRecord(in.ev[k], st), "hipEventRecord");
+                HIP_CHECK(hipStreamWaitEvent(xs, in.ev[k], 0), "hipStreamWaitEvent");
+                BJ_CHECK(all_gather(comm, mine, coeffs + (size_t)r.c0 * n, (size_t)r.count * n * 8, xs));
+                HIP_CHECK(hipEventRecord(arrived.ev[k], xs), "hipEventRecord");
+            }
+        }
+    }
+    // 2. per arrived chunk: this rank's leaf range of its columns' LDE, absorbed into the sponges
+    for (size_t k = 0; k < K; k++) {
+        const Run& r = runs[k];
+        const uint32_t cc = r.c1 - r.c0;
+        uint64_t* out = lde + (size_t)r.c0 * m;
+        if (world > 1) HIP_CHECK(hipStreamWaitEvent(st, arrived.ev[k], 0), "hipStreamWaitEvent");
+        if (fold)
+            BJ_CHECK(bj_lde_shard_folded_d(folded + (size_t)r.c0 * m, cc, m, log_n, log_lde, log_g, rank, out, st));
+        else
+            BJ_CHECK(bj_lde_shard_d(coeffs + (size_t)r.c0 * n, cc, n, log_n, log_lde, log_g, rank, nullptr, out, st));
+        const bool last = k + 1 == K;
+        const uint64_t* cin = k == 0 ? nullptr : state;
+        uint64_t* dst = last ? leaves : state;
+        if (hasher == BJ_HASHER_POSEIDON2)
+            BJ_CHECK(bj_merkle_leaves_partial_d(out, cc, m, m, cin, dst, last ? 1 : 0, st));
+        else if (hasher == BJ_HASHER_BLAKE2S)
+            BJ_CHECK(bj_blake2s_leaves_partial_d(out, cc, m, m, r.c0, cin, dst, last ? 1 : 0, st));
+        else
+            BJ_CHECK(bj_keccak256_leaves_d(out, cc, m, m, dst, st));
+    }
+    // 3. this rank's subtree, then the cap
+    BJ_CHECK(nodes_for(hasher, leaves, m, cap_local, nodes, st));
+    const uint64_t* local_cap = nodes + (m - 2 * (size_t)cap_local) * 4;
+    if (cap_size >= world) {
+        BJ_CHECK(all_gather(comm, local_cap, cap, (size_t)cap_local * 32, st));
+    } else {
+        // fewer cap digests than ranks: gather the subtree roots, hash the top levels everywhere
+        uint64_t *roots = nullptr, *top = nullptr;
+        HIP_CHECK(ws.alloc(&roots, (size_t)world * 4), "hipMallocAsync");
+        HIP_CHECK(ws.alloc(&top, (size_t)(world - cap_size) * 4), "hipMallocAsync");
+        BJ_CHECK(all_gather(comm, local_cap, roots, 32, st));
+        BJ_CHECK(nodes_for(hasher, roots, world, cap_size, top, st));
+        HIP_CHECK(hipMemcpyAsync(cap, top + (size_t)(world - 2 * cap_size) * 4, (size_t)cap_size * 32,
+                                 hipMemcpyDeviceToDevice, st),
+                  "memcpy cap");
+    }
+    return BJ_OK;
+}
+
+}  // extern "C"

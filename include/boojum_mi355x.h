@@ -255,6 +255,62 @@ int bj_lde_commit_h(const uint64_t* trace_h, uint32_t n_cols, uint32_t log_n, ui
                     uint32_t cap_size, uint64_t* lde_h, uint64_t* leaves_h, uint64_t* nodes_h,
                     uint64_t* cap_h);
 
+/* ------------------------------------- collective sharded commit (8(b), 8(e)) */
+/* The whole G-rank witness commitment as one collective call per rank: one process (or
+ * thread) per GPU, each calling bj_sharded_commit_d on its own column shard with its own
+ * communicator.  It runs the column pipeline of DESIGN.md section 7 natively: local iNTTs,
+ * per-chunk exchange on a high-priority stream (G <= D: all-gather of coefficients; G > D:
+ * sender-side fold + all-to-all), this rank's coset/sub-coset LDE, the chained leaf sponge,
+ * the subtree and the cap all-gather.  It replaces MerkleTreeWithCap::construct over
+ * transform_raw_storages_to_lde (utils.rs:270-403, merkle_tree.rs:78-172, prover.rs:313-353)
+ * with the leaf domain split over the ranks.
+ *
+ * Communicators (opaque bj_comm):
+ *   bj_comm_rccl_unique_id  ncclGetUniqueId (128 bytes); rank 0 creates it and the caller
+ *                           broadcasts it by its own means (torch.distributed, MPI, a file);
+ *   bj_comm_init_rccl       ncclCommInitRank on the current device (collective, blocking);
+ *   bj_comm_wrap_rccl       an ncclComm_t the caller already owns (not destroyed by us);
+ *   bj_comm_local_*         in-process ranks that share one device (threads; device-to-device
+ *                           copies through a host barrier): a rehearsal transport that runs the
+ *                           same pipeline multi-rank on one GPU.  Not for performance.
+ * RCCL is resolved at run time (dlopen of librccl.so.1, reusing an already loaded copy), so the
+ * library loads without it.  All ranks must call collectives in the same order. */
+typedef struct bj_comm bj_comm;
+int bj_comm_rccl_unique_id(uint8_t* id_out128);
+int bj_comm_init_rccl(const uint8_t* id128, int world, int rank, bj_comm** out);
+int bj_comm_wrap_rccl(void* nccl_comm, int world, int rank, bj_comm** out);
+int bj_comm_local_group_create(int world, void** group_out);
+int bj_comm_local_group_destroy(void* group);
+int bj_comm_init_local(void* group, int rank, bj_comm** out);
+int bj_comm_destroy(bj_comm* comm);
+
+#define BJ_HASHER_POSEIDON2 0
+#define BJ_HASHER_BLAKE2S 1
+#define BJ_HASHER_KECCAK256 2
+
+/* Which global trace columns rank `shard` of G = 2^log_shards holds, in the order of its
+ * trace_shard rows: the column pipeline deals chunk k (G * c_k consecutive columns, c = u, u,
+ * 2u, 4u, ... capped at 32 rounded to u, u = 8 / gcd(8, G)) as G runs of c_k; when n_cols / G
+ * is not a multiple of u, or the hasher cannot be continued over column ranges (Keccak256),
+ * rank P holds columns [P * n_cols / G, (P + 1) * n_cols / G).  cols_out: n_cols / G entries.
+ * Host only (no device call). */
+int bj_sharded_columns(uint32_t n_cols, uint32_t log_shards, uint32_t shard, int hasher, uint32_t* cols_out);
+
+/* Rank P's part of the G-way commit (G = the communicator's world, a power of two; P its rank).
+ * trace_shard: n_cols / G columns of n = 2^log_n in bj_sharded_columns order at
+ *              trace_shard + j * trace_stride (device, read only).
+ * Outputs (device, this rank's shard of the reference's tree; m = n * 2^log_lde / G leaves,
+ * flat leaf range [P * m, (P + 1) * m) of coset * n + row):
+ *   lde    n_cols x m, global column c at lde + c * m;
+ *   leaves m x 4;
+ *   nodes  (m - cap_local) x 4, the subtree levels, cap_local = max(1, cap_size / G);
+ *   cap    cap_size x 4, the full gathered cap (identical on every rank).
+ * Requires n_cols % G == 0, log_lde >= 1, power-of-two cap_size < n * D, m > cap_local.
+ * Asynchronous on `stream`; workspace comes from the stream-ordered pool. */
+int bj_sharded_commit_d(bj_comm* comm, const uint64_t* trace_shard, size_t trace_stride, uint32_t n_cols,
+                        uint32_t log_n, uint32_t log_lde, uint32_t cap_size, int hasher, uint64_t* lde,
+                        uint64_t* leaves, uint64_t* nodes, uint64_t* cap, void* stream);
+
 /* ------------------------------------------------------------------- FRI */
 
 /* One FRI fold by 2 of a GoldilocksExt2 codeword stored as base columns c0, c1 of n_src

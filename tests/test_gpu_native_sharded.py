@@ -1,0 +1,160 @@
+"""GPU parity of the native collective commit (bj_sharded_commit_d).
+
+G ranks run as G threads on one card with the in-process transport (bj_comm_local_*), which
+drives exactly the native pipeline (chunked exchange on a second stream, per-chunk LDE and
+sponge continuation, subtree, cap gather) with device-to-device copies in place of RCCL.
+Every rank's LDE slice, leaves, subtree levels and cap must equal the oracle's single-process
+commit, bit for bit.  The RCCL transport itself is exercised at world 1 here (one GPU per rank
+is needed beyond that; bench.py --native runs it at N > 1)."""
+import ctypes
+import threading
+
+import numpy as np
+import pytest
+
+import oracle as O
+
+pytestmark = pytest.mark.gpu
+
+
+@pytest.fixture(scope="module")
+def torch_mod():
+    import torch
+    assert torch.cuda.is_available(), "gpu tests need a GPU"
+    import boojum_amd
+    boojum_amd.load()
+    return torch
+
+
+def reference(n_cols, log_n, log_lde, cap, hasher):
+    x = O.synthetic_trace(n_cols, log_n)
+    nl = 1 << (log_n + log_lde)
+    if hasher == "poseidon2":
+        ref = O.lde_commit(x, log_lde, cap, threads=8)
+    else:
+        _, lde = O.lde(x, log_lde, threads=8)
+        leaves, nodes, _, cap_ref = O.merkle_construct(lde.reshape(n_cols, nl), cap, threads=8, hasher=hasher)
+        ref = {"lde": lde, "leaves": leaves, "nodes": nodes, "cap": cap_ref}
+    ref["lde"] = ref["lde"].reshape(n_cols, nl)
+    return ref
+
+
+def check_rank(ref, P, world, cap, lde, leaves, nodes, cap_got):
+    nl = ref["lde"].shape[1]
+    m = nl // world
+    assert np.array_equal(lde, ref["lde"][:, P * m:(P + 1) * m]), "rank %d lde" % P
+    assert np.array_equal(leaves, ref["leaves"][P * m:(P + 1) * m]), "rank %d leaves" % P
+    assert np.array_equal(cap_got, ref["cap"]), "rank %d cap" % P
+    # local subtree level k is the P-th slice of global level k
+    glob_off, o, k = [], 0, 1
+    while (nl >> k) >= cap:
+        glob_off.append(o)
+        o += nl >> k
+        k += 1
+    lo, k = 0, 1
+    while (m >> k) >= max(1, cap // world):
+        cnt = m >> k
+        want = ref["nodes"][glob_off[k - 1] + P * cnt: glob_off[k - 1] + (P + 1) * cnt]
+        assert np.array_equal(nodes[lo:lo + cnt], want), "rank %d node level %d" % (P, k)
+        lo += cnt
+        k += 1
+    assert lo == nodes.shape[0]
+
+
+def run_local(torch, world, n_cols, log_n, log_lde, cap, hasher):
+    from boojum_amd._lib import call
+    from boojum_amd.field import stream_of, to_host
+    from boojum_amd.sharded import LocalGroup, native_columns, native_sharded_commit
+    n = 1 << log_n
+    trace = torch.empty((n_cols, n), dtype=torch.int64, device="cuda")
+    call("bj_fill_synthetic_d", trace.data_ptr(), n_cols, n, log_n, 42, 0, stream_of(trace))
+    torch.cuda.synchronize()
+    group = LocalGroup(world)
+    outs, errors = [None] * world, []
+
+    def rank_main(P):
+        try:
+            torch.cuda.set_device(0)
+            s = torch.cuda.Stream()
+            with torch.cuda.stream(s):
+                cols = torch.tensor(native_columns(n_cols, world, P, hasher), device="cuda")
+                shard = trace.index_select(0, cols).contiguous()
+                comm = group.comm(P)
+                r = native_sharded_commit(comm, shard, n_cols, log_n, log_lde, cap, hasher)
+                s.synchronize()
+                outs[P] = tuple(to_host(t) for t in (r.lde, r.leaves, r.nodes, r.cap))
+                comm.close()
+        except Exception as e:  # noqa: BLE001 - reported below
+            errors.append((P, repr(e)))
+
+    threads = [threading.Thread(target=rank_main, args=(P,), daemon=True) for P in range(world)]
+    for t in threads:
+        t.start()
+    for t in threads:
+        t.join(timeout=120)
+    assert not any(t.is_alive() for t in threads), "a rank did not finish"
+    group.close()
+    assert not errors, errors
+    return outs
+
+
+@pytest.mark.parametrize("world,cfg", [
+    (1, (16, 13, 1, 16, "poseidon2")),
+    (2, (16, 13, 1, 16, "poseidon2")),   # G == D, pipelined (4, 4 columns per rank)
+    (4, (16, 13, 1, 16, "poseidon2")),   # G > D: sender-side fold + all-to-all
+    (8, (32, 13, 2, 4, "poseidon2")),    # G > D, cap < G: roots gathered, top levels everywhere
+    (2, (32, 13, 2, 16, "poseidon2")),   # G < D: whole cosets
+    (8, (24, 12, 2, 16, "poseidon2")),   # 3 columns per rank, chunks 1, 1, 1; DIF-size NTT
+    (4, (12, 13, 1, 16, "poseidon2")),   # 3 columns per rank (not a multiple of 2): one chunk
+    (8, (256, 13, 2, 16, "poseidon2")),  # C3's column deal at G = 8 (1, 1, 2, 4, 8, 16 per rank)
+    (2, (16, 13, 2, 16, "blake2s")),     # chaining value carried across chunks
+    (8, (16, 13, 1, 4, "blake2s")),
+    (4, (16, 13, 1, 8, "keccak256")),    # no continuation: one chunk
+])
+def test_native_sharded_commit_local_ranks(torch_mod, world, cfg):
+    n_cols, log_n, log_lde, cap, hasher = cfg
+    outs = run_local(torch_mod, world, n_cols, log_n, log_lde, cap, hasher)
+    ref = reference(n_cols, log_n, log_lde, cap, hasher)
+    for P in range(world):
+        check_rank(ref, P, world, cap, *outs[P])
+
+
+def test_native_sharded_commit_rccl_world1(torch_mod):
+    """The RCCL transport end to end at world 1 (ncclCommInitRank with one rank)."""
+    torch = torch_mod
+    from boojum_amd._lib import call, check, load
+    from boojum_amd.field import stream_of, to_host
+    from boojum_amd.sharded import NativeComm, native_sharded_commit
+    n_cols, log_n, log_lde, cap = 16, 13, 2, 16
+    L = load()
+    uid = (ctypes.c_uint8 * 128)()
+    check(L.bj_comm_rccl_unique_id(uid), "unique id")
+    comm = NativeComm._make("bj_comm_init_rccl", uid, 1, 0, world=1, rank=0)
+    try:
+        trace = torch.empty((n_cols, 1 << log_n), dtype=torch.int64, device="cuda")
+        call("bj_fill_synthetic_d", trace.data_ptr(), n_cols, 1 << log_n, log_n, 42, 0, stream_of(trace))
+        r = native_sharded_commit(comm, trace, n_cols, log_n, log_lde, cap)
+        torch.cuda.synchronize()
+        ref = reference(n_cols, log_n, log_lde, cap, "poseidon2")
+        check_rank(ref, 0, 1, cap, to_host(r.lde), to_host(r.leaves), to_host(r.nodes), to_host(r.cap))
+    finally:
+        comm.close()
+
+
+def test_native_sharded_commit_rejects_bad_shapes(torch_mod):
+    torch = torch_mod
+    from boojum_amd._lib import BoojumError
+    from boojum_amd.sharded import LocalGroup, NativeShardedResult, native_sharded_commit
+    group = LocalGroup(2)
+    comm = group.comm(0)
+    try:
+        out = NativeShardedResult(4, 8, 1, 4, 2)
+        with pytest.raises(BoojumError):   # cap_size not a power of two
+            native_sharded_commit(comm, torch.zeros((2, 256), dtype=torch.int64, device="cuda"), 4, 8, 1, 3,
+                                  out=out)
+        with pytest.raises(BoojumError):   # lde degree 1
+            native_sharded_commit(comm, torch.zeros((2, 256), dtype=torch.int64, device="cuda"), 4, 8, 0, 4,
+                                  out=out)
+    finally:
+        comm.close()
+        group.close()
