@@ -25,6 +25,7 @@
 #include <string.h>
 
 #include "boojum_mi355x.h"
+#include <hip/hip_runtime_api.h> /* device buffers for the *_d family (a Rust host: hip-sys) */
 
 typedef uint64_t u64;
 #define GL_P 0xFFFFFFFF00000001ull
@@ -184,7 +185,98 @@ static void check_commit(uint32_t log_n, uint32_t n_cols, uint32_t log_lde, uint
     free(trace); free(lde); free(leaves); free(nodes); free(r_lde); free(r_leaves); free(r_nodes);
 }
 
-/* ------------------------------------------------------------ 4. error contract */
+/* ------------------------------- 4. collective sharded commit, one thread per rank */
+
+typedef struct {
+    void* group;
+    int rank, world;
+    uint32_t n_cols, log_n, log_lde, cap;
+    const u64* trace; /* all columns, host */
+    u64* leaves;      /* all leaves, host: rank P writes its range */
+    u64* cap_out;     /* this rank's gathered cap */
+    int rc;
+} rank_job_t;
+
+#define HIPC(expr)                                     \
+    do {                                               \
+        if ((expr) != hipSuccess) {                    \
+            fprintf(stderr, "HIP error: %s\n", #expr); \
+            j->rc = -1;                                \
+            return NULL;                               \
+        }                                              \
+    } while (0)
+
+/* What one rank of a multi-GPU prover does: its columns (bj_sharded_columns order) into HBM,
+ * then one collective bj_sharded_commit_d.  Ranks share one device through the in-process
+ * transport here; with RCCL each would own a GPU (bj_comm_init_rccl). */
+static void* rank_worker(void* p) {
+    rank_job_t* j = (rank_job_t*)p;
+    const size_t n = (size_t)1 << j->log_n, nl = n << j->log_lde, m = nl / j->world;
+    const uint32_t cpr = j->n_cols / j->world, cap_local = j->cap / j->world ? j->cap / j->world : 1;
+    uint32_t log_g = 0;
+    while ((1 << log_g) < j->world) log_g++;
+    uint32_t* cols = xmalloc(4 * cpr);
+    j->rc = bj_sharded_columns(j->n_cols, log_g, j->rank, BJ_HASHER_POSEIDON2, cols);
+    if (j->rc) return NULL;
+    HIPC(hipSetDevice(0));
+    hipStream_t st;
+    HIPC(hipStreamCreate(&st));
+    u64 *tr, *lde, *leaves, *nodes, *cap;
+    HIPC(hipMalloc((void**)&tr, 8 * n * cpr));
+    HIPC(hipMalloc((void**)&lde, 8 * m * j->n_cols));
+    HIPC(hipMalloc((void**)&leaves, 32 * m));
+    HIPC(hipMalloc((void**)&nodes, 32 * (m - cap_local)));
+    HIPC(hipMalloc((void**)&cap, 32 * j->cap));
+    for (uint32_t c = 0; c < cpr; c++) HIPC(hipMemcpy(tr + c * n, j->trace + (size_t)cols[c] * n, 8 * n, hipMemcpyHostToDevice));
+    bj_comm* comm = NULL;
+    j->rc = bj_comm_init_local(j->group, j->rank, &comm);
+    if (j->rc) return NULL;
+    j->rc = bj_sharded_commit_d(comm, tr, n, j->n_cols, j->log_n, j->log_lde, j->cap, BJ_HASHER_POSEIDON2, lde,
+                                leaves, nodes, cap, st);
+    if (j->rc == 0) {
+        HIPC(hipStreamSynchronize(st));
+        HIPC(hipMemcpy(j->leaves + 4 * m * j->rank, leaves, 32 * m, hipMemcpyDeviceToHost));
+        HIPC(hipMemcpy(j->cap_out, cap, 32 * j->cap, hipMemcpyDeviceToHost));
+    }
+    bj_comm_destroy(comm);
+    hipFree(tr); hipFree(lde); hipFree(leaves); hipFree(nodes); hipFree(cap);
+    hipStreamDestroy(st);
+    free(cols);
+    return NULL;
+}
+
+static void check_sharded(uint32_t log_n, uint32_t n_cols, uint32_t log_lde, uint32_t cap, int world) {
+    size_t n = (size_t)1 << log_n, nl = n << log_lde, n_nodes = nl - cap;
+    u64* trace = xmalloc(8 * n * n_cols);
+    for (uint32_t c = 0; c < n_cols; c++)
+        for (size_t r = 0; r < n; r++) trace[(size_t)c * n + r] = canon(splitmix64(42 + (u64)c * n + r));
+    u64* leaves = xmalloc(32 * nl), *caps = xmalloc(32 * (size_t)cap * world);
+    void* group = NULL;
+    int rc = bj_comm_local_group_create(world, &group);
+    CHECK(rc == BJ_OK, "bj_comm_local_group_create: %s", bj_last_error());
+    if (rc) return;
+    pthread_t th[64];
+    rank_job_t jobs[64];
+    for (int P = 0; P < world; P++) {
+        jobs[P] = (rank_job_t){group, P, world, n_cols, log_n, log_lde, cap, trace, leaves, caps + 4 * (size_t)cap * P, 0};
+        pthread_create(&th[P], NULL, rank_worker, &jobs[P]);
+    }
+    for (int P = 0; P < world; P++) {
+        pthread_join(th[P], NULL);
+        CHECK(jobs[P].rc == 0, "rank %d of %d: rc %d", P, world, jobs[P].rc);
+    }
+    bj_comm_local_group_destroy(group);
+    u64* r_lde = xmalloc(8 * nl * n_cols), *r_leaves = xmalloc(32 * nl), *r_nodes = xmalloc(32 * n_nodes);
+    u64 r_cap[4 * 4096];
+    bjo_lde_commit(trace, n_cols, log_n, log_lde, cap, r_lde, r_leaves, r_nodes, r_cap, 4);
+    size_t w = 0;
+    CHECK(eq_canon(leaves, r_leaves, 4 * nl, &w), "sharded x%d leaves differ at %zu", world, w);
+    for (int P = 0; P < world; P++)
+        CHECK(eq_canon(caps + 4 * (size_t)cap * P, r_cap, 4 * cap, &w), "sharded x%d: rank %d cap differs", world, P);
+    free(trace); free(leaves); free(caps); free(r_lde); free(r_leaves); free(r_nodes);
+}
+
+/* ------------------------------------------------------------ 5. error contract */
 
 static void check_errors(void) {
     u64 col[12] = {0};
@@ -210,6 +302,9 @@ int main(int argc, char** argv) {
     check_tree_hasher();
     u64 cap_out[4 * 4096];
     check_commit(log_n, n_cols, log_lde, cap, threads, cap_out);
+    for (int world = 2; world <= 8; world *= 2)
+        if (n_cols % world == 0 && ((size_t)1 << (log_n + log_lde)) / world > (cap / world ? cap / world : 1))
+            check_sharded(log_n, n_cols, log_lde, cap, world);
     check_errors();
     if (failures) {
         fprintf(stderr, "%d check(s) failed\n", failures);
