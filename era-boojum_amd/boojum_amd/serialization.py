@@ -101,3 +101,48 @@ def read_merkle_tree(f):
     n = _read_u64(f)
     levels = [read_digests(f) for _ in range(n)]
     return cap_size, leaves, levels
+
+
+# ------------------------------------------------------------- serde JSON (proof format)
+# The prover's Proof is serde-serialised (cs/implementations/proof.rs:118-160); the parts this
+# path produces are caps (MerkleTreeCap = Vec<[F; 4]>) and OracleQuery {leaf_elements: Vec<F>,
+# proof: Vec<[F; 4]>} (proof.rs:48-63).  GoldilocksField serialises as its u64 (canonical here),
+# so proof.json holds plain integers: a cap is [[u64; 4], ...], a query
+# {"leaf_elements": [...], "proof": [[u64; 4], ...]}.
+
+def _canon_list(a):
+    a = _host(a).astype(np.uint64)
+    p = np.uint64(0xFFFFFFFF00000001)
+    a = np.where(a >= p, a - p, a)
+    return a.tolist()
+
+
+def cap_to_json(cap):
+    """MerkleTreeCap -> list of 4-lists of canonical ints (as in proof.json's *_oracle_cap)."""
+    return _canon_list(np.asarray(_host(cap)).reshape(-1, 4))
+
+
+def cap_from_json(obj):
+    a = np.asarray(obj, dtype=np.uint64)
+    if a.ndim != 2 or a.shape[1] != 4:
+        raise ValueError("a cap is a list of 4-element digests")
+    return a
+
+
+def oracle_query_to_json(leaf_elements, proof):
+    """OracleQuery -> {"leaf_elements": [...], "proof": [[...], ...]} (serde field order)."""
+    return {"leaf_elements": _canon_list(np.asarray(_host(leaf_elements)).reshape(-1)),
+            "proof": _canon_list(np.asarray(_host(proof)).reshape(-1, 4))}
+
+
+def oracle_query_from_json(obj):
+    """-> (leaf_elements (k,), proof (depth, 4)) as numpy uint64."""
+    leaf = np.asarray(obj["leaf_elements"], dtype=np.uint64).reshape(-1)
+    proof = np.asarray(obj["proof"], dtype=np.uint64).reshape(-1, 4)
+    return leaf, proof
+
+
+def dumps(obj):
+    """serde_json::to_string layout: no whitespace."""
+    import json
+    return json.dumps(obj, separators=(",", ":"))
