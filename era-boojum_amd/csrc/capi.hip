@@ -827,168 +827,6 @@ int bj_keccak256_node_h(const uint64_t* left4, const uint64_t* right4, uint64_t*
     return BJ_OK;
 }
 
-int bj_lde_commit_h(const uint64_t* trace_h, uint32_t n_cols, uint32_t log_n, uint32_t log_lde, uint32_t cap_size,
-                    uint64_t* lde_h, uint64_t* leaves_h, uint64_t* nodes_h, uint64_t* cap_h) {
-    if (int r = check_log_n(log_n + log_lde)) return r;
-    const size_t n = (size_t)1 << log_n, nl = n << log_lde;
-    const uint32_t D = 1u << log_lde;
-    if (!is_pow2(cap_size) || nl <= cap_size) return fail(BJ_EINVAL, "need power-of-two cap_size < n * D");
-    if (log_lde == 0) return fail(BJ_EINVAL, "lde degree must be > 1 (utils.rs:283)");
-    // Column-chunked pipeline over host buffers: the trace of chunk k+1 goes in (this thread)
-    // while chunk k is transformed and absorbed into the leaf sponges (compute stream) and the
-    // LDE of chunk k-1 comes out (a copy-out thread), so both PCIe directions and the GPU work
-    // at once.  Chunks are 32 columns (a multiple of the sponge rate), the leaf sponges carry
-    // their capacity words between chunks (bj_merkle_leaves_partial_d); outputs equal the
-    // one-shot commit.  Device buffers come from the stream-ordered pool (reused across calls).
-    const uint32_t KC = 32;
-    const uint32_t n_chunks = n_cols ? (n_cols + KC - 1) / KC : 0;
-    // three streams per calling thread and device, created once (stream creation costs
-    // milliseconds on ROCm); calls from one thread are sequential, so reuse is safe
-    struct HostStreams {
-        int dev = -1;
-        hipStream_t s[3] = {nullptr, nullptr, nullptr};
-    };
-    thread_local std::map<int, HostStreams> tl_streams;
-    int cur_dev = 0;
-    HIP_TRY(hipGetDevice(&cur_dev), "hipGetDevice");
-    HostStreams& hs = tl_streams[cur_dev];
-    if (hs.dev != cur_dev) {
-        for (auto& s : hs.s) HIP_TRY(hipStreamCreateWithFlags(&s, hipStreamNonBlocking), "hipStreamCreate");
-        hs.dev = cur_dev;
-    }
-    hipStream_t s_in = hs.s[0], s_cmp = hs.s[1], s_out = hs.s[2];
-    {
-        // keep freed pool memory mapped between calls: without this the stream-ordered pool
-        // returns it to the driver at every synchronisation and the next call re-maps the
-        // whole workspace (~20 ms for C2's 5 GB)
-        int dev0 = 0;
-        hipMemPool_t pool;
-        HIP_TRY(hipGetDevice(&dev0), "hipGetDevice");
-        HIP_TRY(hipDeviceGetDefaultMemPool(&pool, dev0), "hipDeviceGetDefaultMemPool");
-        uint64_t keep = UINT64_MAX;
-        HIP_TRY(hipMemPoolSetAttribute(pool, hipMemPoolAttrReleaseThreshold, &keep), "hipMemPoolSetAttribute");
-    }
-    const size_t tn = n * n_cols;
-    uint64_t *tr = nullptr, *mono = nullptr, *lde = nullptr, *lv = nullptr, *nd = nullptr, *st = nullptr;
-    HIP_TRY(hipMallocAsync((void**)&tr, (tn ? tn : 1) * 8, s_cmp), "hipMallocAsync");
-    HIP_TRY(hipMallocAsync((void**)&mono, (tn ? tn : 1) * 8, s_cmp), "hipMallocAsync");
-    HIP_TRY(hipMallocAsync((void**)&lde, (tn ? tn << log_lde : 1) * 8, s_cmp), "hipMallocAsync");
-    HIP_TRY(hipMallocAsync((void**)&lv, nl * 32, s_cmp), "hipMallocAsync");
-    HIP_TRY(hipMallocAsync((void**)&nd, (nl - cap_size) * 32, s_cmp), "hipMallocAsync");
-    HIP_TRY(hipMallocAsync((void**)&st, nl * 32, s_cmp), "hipMallocAsync");
-    HIP_TRY(hipStreamSynchronize(s_cmp), "sync");
-    struct Frees {
-        uint64_t** p[6];
-        hipStream_t s;
-        ~Frees() {
-            for (auto q : p)
-                if (*q) (void)hipFreeAsync(*q, s);
-            (void)hipStreamSynchronize(s);
-        }
-    } frees{{&tr, &mono, &lde, &lv, &nd, &st}, s_cmp};
-    std::vector<hipEvent_t> ev_in(n_chunks), ev_cmp(n_chunks);
-    struct Events {
-        std::vector<hipEvent_t>* v[2];
-        ~Events() {
-            for (auto e : v)
-                for (auto x : *e)
-                    if (x) (void)hipEventDestroy(x);
-        }
-    } evg{{&ev_in, &ev_cmp}};
-    for (uint32_t k = 0; k < n_chunks; k++) {
-        ev_in[k] = ev_cmp[k] = nullptr;
-        HIP_TRY(hipEventCreateWithFlags(&ev_in[k], hipEventDisableTiming), "hipEventCreate");
-        HIP_TRY(hipEventCreateWithFlags(&ev_cmp[k], hipEventDisableTiming), "hipEventCreate");
-    }
-    // copy-out thread: the LDE rows of chunk k as soon as its compute is done.  It waits on the
-    // host until this thread has recorded ev_cmp[k] (an unrecorded event counts as complete),
-    // and stops early when the issuing side fails.
-    hipError_t out_err = hipSuccess;
-    std::mutex mu;
-    std::condition_variable cv;
-    uint32_t recorded = 0;
-    bool abort_out = false;
-    int dev = 0;
-    HIP_TRY(hipGetDevice(&dev), "hipGetDevice");
-    std::thread out_thread([&]() {
-        (void)hipSetDevice(dev);
-        for (uint32_t k = 0; k < n_chunks && out_err == hipSuccess; k++) {
-            {
-                std::unique_lock<std::mutex> lk(mu);
-                cv.wait(lk, [&] { return recorded > k || abort_out; });
-                if (recorded <= k) return;
-            }
-            const uint32_t c0 = k * KC, c = std::min(KC, n_cols - c0);
-            hipError_t e = hipEventSynchronize(ev_cmp[k]);
-            if (e == hipSuccess && lde_h)
-                e = hipMemcpyAsync(lde_h + (size_t)c0 * nl, lde + (size_t)c0 * nl, (size_t)c * nl * 8,
-                                   hipMemcpyDeviceToHost, s_out);
-            if (e == hipSuccess) e = hipStreamSynchronize(s_out);
-            if (e != hipSuccess) out_err = e;
-        }
-    });
-    struct Join {
-        std::thread* t;
-        std::mutex* mu;
-        std::condition_variable* cv;
-        bool* abort_out;
-        ~Join() {
-            {
-                std::lock_guard<std::mutex> lk(*mu);
-                *abort_out = true;
-            }
-            cv->notify_all();
-            if (t->joinable()) t->join();
-        }
-    } join{&out_thread, &mu, &cv, &abort_out};
-    for (uint32_t k = 0; k < n_chunks; k++) {
-        const uint32_t c0 = k * KC, c = std::min(KC, n_cols - c0);
-        const bool last = k + 1 == n_chunks;
-        HIP_TRY(hipMemcpyAsync(tr + (size_t)c0 * n, trace_h + (size_t)c0 * n, (size_t)c * n * 8,
-                               hipMemcpyHostToDevice, s_in),
-                "memcpy");
-        HIP_TRY(hipEventRecord(ev_in[k], s_in), "hipEventRecord");
-        HIP_TRY(hipStreamWaitEvent(s_cmp, ev_in[k], 0), "hipStreamWaitEvent");
-        if (int r = bj_lde_d(tr + (size_t)c0 * n, c, n, log_n, log_lde, mono + (size_t)c0 * n, lde + (size_t)c0 * nl,
-                             s_cmp))
-            return r;
-        if (int r = bj_merkle_leaves_partial_d(lde + (size_t)c0 * nl, c, nl, nl, k ? st : nullptr, last ? lv : st,
-                                               last ? 1 : 0, s_cmp))
-            return r;
-        HIP_TRY(hipEventRecord(ev_cmp[k], s_cmp), "hipEventRecord");
-        {
-            std::lock_guard<std::mutex> lk(mu);
-            recorded = k + 1;
-        }
-        cv.notify_all();
-    }
-    if (n_chunks == 0)
-        if (int r = bj_merkle_leaves_d(lde, 0, nl, nl, lv, s_cmp)) return r;
-    hipEvent_t ev_leaves = nullptr;
-    HIP_TRY(hipEventCreateWithFlags(&ev_leaves, hipEventDisableTiming), "hipEventCreate");
-    struct Ev {
-        hipEvent_t* e;
-        ~Ev() { (void)hipEventDestroy(*e); }
-    } evl{&ev_leaves};
-    HIP_TRY(hipEventRecord(ev_leaves, s_cmp), "hipEventRecord");
-    if (int r = bj_merkle_nodes_d(lv, nl, cap_size, nd, s_cmp)) return r;
-    out_thread.join();
-    if (out_err != hipSuccess) return hip_fail(out_err, "memcpy lde");
-    // the leaf digests go out while the node levels are hashed
-    if (leaves_h) {
-        HIP_TRY(hipStreamWaitEvent(s_out, ev_leaves, 0), "hipStreamWaitEvent");
-        HIP_TRY(hipMemcpyAsync(leaves_h, lv, nl * 32, hipMemcpyDeviceToHost, s_out), "memcpy");
-    }
-    HIP_TRY(hipStreamSynchronize(s_cmp), "sync");
-    if (nodes_h) HIP_TRY(hipMemcpyAsync(nodes_h, nd, (nl - cap_size) * 32, hipMemcpyDeviceToHost, s_cmp), "memcpy");
-    if (cap_h)
-        HIP_TRY(hipMemcpyAsync(cap_h, nd + 4 * (nl - 2 * (size_t)cap_size), (size_t)cap_size * 32,
-                               hipMemcpyDeviceToHost, s_cmp),
-                "memcpy");
-    HIP_TRY(hipStreamSynchronize(s_cmp), "sync");
-    HIP_TRY(hipStreamSynchronize(s_out), "sync");
-    (void)D;
-    return BJ_OK;
-}
+// bj_lde_commit_h: host_commit.hip
 
 }  // extern "C"
