@@ -67,6 +67,8 @@ SIGNATURES = {
     "bj_comm_destroy": ([_vp], _int),
     "bj_sharded_columns": ([_u32, _u32, _u32, _int, ctypes.POINTER(_u32)], _int),
     "bj_sharded_commit_d": ([_vp, _vp, _sz, _u32, _u32, _u32, _u32, _int, _vp, _vp, _vp, _vp, _vp], _int),
+    "bj_sharded_query_h": ([_vp, _vp, _vp, _vp, _u32, _u32, _u32, _u32, _int, _u64, _u64p, _u64p, _u64p, _vp],
+                           _int),
     "bj_fri_fold_d": ([_vp, _vp, _sz, _vp, _u64, _u64, _u64, _vp, _vp, _vp], _int),
     "bj_fill_synthetic_d": ([_vp, _u32, _sz, _u32, _u64, _u64, _vp], _int),
     "bj_gl_op_d": ([_int, _vp, _vp, _vp, _sz, _vp], _int),

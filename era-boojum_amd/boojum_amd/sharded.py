@@ -503,3 +503,19 @@ def native_sharded_commit(comm, trace_shard, n_cols, log_n, log_lde, cap_size, h
          cap_size, HASHER_IDS[hasher], out.lde.data_ptr(), out.leaves.data_ptr(), out.nodes.data_ptr(),
          out.cap.data_ptr(), stream_of(out.lde))
     return out
+
+
+def native_sharded_query(comm, res, n_cols, log_n, log_lde, cap_size, tree_idx, hasher="poseidon2"):
+    """bj_sharded_query_h: OracleQuery::construct on a native sharded commit (res is this rank's
+    NativeShardedResult).  Collective over `comm`; every rank returns the same
+    (leaf_elements (C,), leaf_hash (4,), proof (depth, 4)) as numpy uint64."""
+    import ctypes
+    import numpy as np
+    depth = (log_n + log_lde) - _log2(cap_size)
+    elems = np.zeros(n_cols, dtype=np.uint64)
+    leaf = np.zeros(4, dtype=np.uint64)
+    proof = np.zeros((max(depth, 1), 4), dtype=np.uint64)
+    p = lambda a: a.ctypes.data_as(ctypes.POINTER(ctypes.c_uint64))  # noqa: E731
+    call("bj_sharded_query_h", comm.handle, res.lde.data_ptr(), res.leaves.data_ptr(), res.nodes.data_ptr(), n_cols,
+         log_n, log_lde, cap_size, HASHER_IDS[hasher], tree_idx, p(elems), p(leaf), p(proof), stream_of(res.lde))
+    return elems, leaf, proof[:depth]

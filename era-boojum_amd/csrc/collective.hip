@@ -515,4 +515,74 @@ int bj_sharded_commit_d(bj_comm* comm, const uint64_t* trace_shard, size_t trace
     return BJ_OK;
 }
 
+int bj_sharded_query_h(bj_comm* comm, const uint64_t* lde, const uint64_t* leaves, const uint64_t* nodes,
+                       uint32_t n_cols, uint32_t log_n, uint32_t log_lde, uint32_t cap_size, int hasher, uint64_t idx,
+                       uint64_t* leaf_elements_h, uint64_t* leaf_hash_h, uint64_t* proof_h, void* stream) {
+    if (!comm) return err(BJ_EINVAL, "null communicator");
+    if (hasher < BJ_HASHER_POSEIDON2 || hasher > BJ_HASHER_KECCAK256) return err(BJ_EINVAL, "unknown hasher");
+    const uint32_t world = (uint32_t)comm->world, rank = (uint32_t)comm->rank;
+    const uint32_t log_g = log2u(world);
+    if (log_n > 30 || log_g > log_n + log_lde || n_cols == 0) return err(BJ_EINVAL, "bad geometry");
+    const size_t nl = (size_t)1 << (log_n + log_lde), m = nl >> log_g;
+    if (!is_pow2(cap_size) || nl <= cap_size) return err(BJ_EINVAL, "need power-of-two cap_size < n * D");
+    const uint32_t cap_local = std::max<uint32_t>(1, cap_size / world);
+    if (m <= cap_local) return err(BJ_EINVAL, "each shard needs more leaves than its cap slice");
+    if (idx >= nl) return err(BJ_EINVAL, "tree index out of range");
+    if (!lde || !leaves || !nodes || !leaf_elements_h || !leaf_hash_h || !proof_h) return err(BJ_EINVAL, "null buffer");
+    hipStream_t st = reinterpret_cast<hipStream_t>(stream);
+    const uint32_t owner = (uint32_t)(idx / m);
+    const size_t local = idx % m;
+    const uint32_t local_depth = log2u(m) - log2u(cap_local);
+    const uint32_t top_depth = cap_size < world ? log_g - log2u(cap_size) : 0;
+    const size_t words = (size_t)n_cols + 4 + 4 * ((size_t)local_depth + top_depth);
+    Workspace ws(st);
+    uint64_t *buf = nullptr, *all = nullptr;
+    HIP_CHECK(ws.alloc(&buf, words), "hipMallocAsync");
+    HIP_CHECK(ws.alloc(&all, words * world), "hipMallocAsync");
+    HIP_CHECK(hipMemsetAsync(buf, 0, words * 8, st), "memset");
+    if (rank == owner) {
+        // leaf_elements: every column's LDE value at the row (a strided gather), then the leaf
+        HIP_CHECK(hipMemcpy2DAsync(buf, 8, lde + local, m * 8, 8, n_cols, hipMemcpyDeviceToDevice, st), "gather row");
+        HIP_CHECK(hipMemcpyAsync(buf + n_cols, leaves + 4 * local, 32, hipMemcpyDeviceToDevice, st), "leaf");
+        // siblings up the subtree (MerkleTreeWithCap::get_proof, merkle_tree.rs:462-480); node
+        // level l >= 1 holds m >> l digests after the lower levels
+        size_t at = local, level_off = 0, level_len = m;
+        for (uint32_t l = 0; l < local_depth; l++) {
+            const uint64_t* src = l == 0 ? leaves + 4 * (at ^ 1) : nodes + 4 * (level_off + (at ^ 1));
+            HIP_CHECK(hipMemcpyAsync(buf + n_cols + 4 + 4 * l, src, 32, hipMemcpyDeviceToDevice, st), "sibling");
+            if (l > 0) level_off += level_len;
+            level_len >>= 1;
+            at >>= 1;
+        }
+    }
+    if (top_depth) {
+        // cap < G: the top levels over the G subtree roots, hashed on every rank
+        uint64_t *roots = nullptr, *top = nullptr;
+        HIP_CHECK(ws.alloc(&roots, (size_t)world * 4), "hipMallocAsync");
+        HIP_CHECK(ws.alloc(&top, (size_t)(world - cap_size) * 4), "hipMallocAsync");
+        BJ_CHECK(all_gather(comm, nodes + (m - 2 * (size_t)cap_local) * 4, roots, 32, st));
+        BJ_CHECK(nodes_for(hasher, roots, world, cap_size, top, st));
+        size_t at = owner, level_off = 0, level_len = world;
+        for (uint32_t l = 0; l < top_depth; l++) {
+            const uint64_t* src = l == 0 ? roots + 4 * (at ^ 1) : top + 4 * (level_off + (at ^ 1));
+            HIP_CHECK(hipMemcpyAsync(buf + n_cols + 4 + 4 * ((size_t)local_depth + l), src, 32,
+                                     hipMemcpyDeviceToDevice, st),
+                      "top sibling");
+            if (l > 0) level_off += level_len;
+            level_len >>= 1;
+            at >>= 1;
+        }
+    }
+    // every rank gets the owner's row and path (the other ranks contributed zeros)
+    BJ_CHECK(all_gather(comm, buf, all, words * 8, st));
+    const uint64_t* mine = all + (size_t)owner * words;
+    HIP_CHECK(hipMemcpyAsync(leaf_elements_h, mine, (size_t)n_cols * 8, hipMemcpyDeviceToHost, st), "memcpy");
+    HIP_CHECK(hipMemcpyAsync(leaf_hash_h, mine + n_cols, 32, hipMemcpyDeviceToHost, st), "memcpy");
+    HIP_CHECK(hipMemcpyAsync(proof_h, mine + n_cols + 4, 32 * ((size_t)local_depth + top_depth), hipMemcpyDeviceToHost,
+                             st),
+              "memcpy");
+    HIP_CHECK(hipStreamSynchronize(st), "sync");
+    return BJ_OK;
+}
+
 }  // extern "C"

@@ -311,6 +311,17 @@ int bj_sharded_commit_d(bj_comm* comm, const uint64_t* trace_shard, size_t trace
                         uint32_t log_n, uint32_t log_lde, uint32_t cap_size, int hasher, uint64_t* lde,
                         uint64_t* leaves, uint64_t* nodes, uint64_t* cap, void* stream);
 
+/* OracleQuery::construct (proof.rs:65-97) on a bj_sharded_commit_d commit: tree index idx (flat
+ * leaf index coset * n + row) of the global tree.  The owning rank reads the row of every
+ * column and its subtree path; when cap_size < G the top levels over the gathered subtree roots
+ * finish the path on every rank.  Collective: every rank passes its own commit outputs and the
+ * same idx, and every rank receives, in host memory, leaf_elements (n_cols), leaf_hash (4) and
+ * proof (depth x 4, depth = log2(n * D / cap_size), MerkleTreeWithCap::get_proof order,
+ * merkle_tree.rs:462-480).  Synchronous. */
+int bj_sharded_query_h(bj_comm* comm, const uint64_t* lde, const uint64_t* leaves, const uint64_t* nodes,
+                       uint32_t n_cols, uint32_t log_n, uint32_t log_lde, uint32_t cap_size, int hasher, uint64_t idx,
+                       uint64_t* leaf_elements_h, uint64_t* leaf_hash_h, uint64_t* proof_h, void* stream);
+
 /* ------------------------------------------------------------------- FRI */
 
 /* One FRI fold by 2 of a GoldilocksExt2 codeword stored as base columns c0, c1 of n_src

@@ -39,7 +39,21 @@ def reference(n_cols, log_n, log_lde, cap, hasher):
     return ref
 
 
-def check_rank(ref, P, world, cap, lde, leaves, nodes, cap_got):
+def check_queries(ref, cap, qs, hasher):
+    """OracleQuery::construct results (every rank the same) against the full tree's proofs."""
+    nl = ref["lde"].shape[1]
+    levels = (nl.bit_length() - 1) - (cap.bit_length() - 1)
+    for idx, (elems, leaf, proof) in zip(query_indices(nl), qs):
+        want_leaf, want_path = O.merkle_get_proof(ref["leaves"], ref["nodes"], levels, idx)
+        assert np.array_equal(elems, ref["lde"][:, idx]), "query %d elements" % idx
+        assert np.array_equal(leaf, want_leaf), "query %d leaf" % idx
+        assert np.array_equal(proof, want_path), "query %d path" % idx
+        assert O.verify_proof_over_cap(proof, ref["cap"], leaf, idx, hasher=hasher)
+
+
+def check_rank(ref, P, world, cap, lde, leaves, nodes, cap_got, qs=None, hasher="poseidon2"):
+    if qs is not None:
+        check_queries(ref, cap, qs, hasher)
     nl = ref["lde"].shape[1]
     m = nl // world
     assert np.array_equal(lde, ref["lde"][:, P * m:(P + 1) * m]), "rank %d lde" % P
@@ -61,10 +75,14 @@ def check_rank(ref, P, world, cap, lde, leaves, nodes, cap_got):
     assert lo == nodes.shape[0]
 
 
+def query_indices(nl):
+    return sorted({0, 1, nl // 2 - 1, nl // 2, nl - 1, (nl * 3) // 7})
+
+
 def run_local(torch, world, n_cols, log_n, log_lde, cap, hasher):
     from boojum_amd._lib import call
     from boojum_amd.field import stream_of, to_host
-    from boojum_amd.sharded import LocalGroup, native_columns, native_sharded_commit
+    from boojum_amd.sharded import LocalGroup, native_columns, native_sharded_commit, native_sharded_query
     n = 1 << log_n
     trace = torch.empty((n_cols, n), dtype=torch.int64, device="cuda")
     call("bj_fill_synthetic_d", trace.data_ptr(), n_cols, n, log_n, 42, 0, stream_of(trace))
@@ -82,7 +100,9 @@ def run_local(torch, world, n_cols, log_n, log_lde, cap, hasher):
                 comm = group.comm(P)
                 r = native_sharded_commit(comm, shard, n_cols, log_n, log_lde, cap, hasher)
                 s.synchronize()
-                outs[P] = tuple(to_host(t) for t in (r.lde, r.leaves, r.nodes, r.cap))
+                qs = [native_sharded_query(comm, r, n_cols, log_n, log_lde, cap, i, hasher)
+                      for i in query_indices(1 << (log_n + log_lde))]
+                outs[P] = tuple(to_host(t) for t in (r.lde, r.leaves, r.nodes, r.cap)) + (qs,)
                 comm.close()
         except Exception as e:  # noqa: BLE001 - reported below
             errors.append((P, repr(e)))
@@ -116,7 +136,7 @@ def test_native_sharded_commit_local_ranks(torch_mod, world, cfg):
     outs = run_local(torch_mod, world, n_cols, log_n, log_lde, cap, hasher)
     ref = reference(n_cols, log_n, log_lde, cap, hasher)
     for P in range(world):
-        check_rank(ref, P, world, cap, *outs[P])
+        check_rank(ref, P, world, cap, *outs[P], hasher=hasher)
 
 
 def test_native_sharded_commit_rccl_world1(torch_mod):
