@@ -100,14 +100,17 @@ class CopyPool {
     unsigned parts_ = 1;
 };
 
-// BJ_COPY_THREADS (default 8) host threads share each staged copy.
-CopyPool& copy_pool() {
-    static CopyPool* p = [] {
+// One pool per direction (the copy-in and copy-out sides run at once and must not queue behind
+// each other), BJ_COPY_THREADS (default 6) threads each, counting the calling thread.
+CopyPool& copy_pool(int dir) {
+    static CopyPool* p[2] = {nullptr, nullptr};
+    static std::once_flag once;
+    std::call_once(once, [] {
         const char* e = std::getenv("BJ_COPY_THREADS");
-        const int t = e ? std::atoi(e) : 8;
-        return new CopyPool((unsigned)std::max(0, std::min(t, 64) - 1));
-    }();
-    return *p;
+        const int t = e ? std::atoi(e) : 6;
+        for (auto& q : p) q = new CopyPool((unsigned)std::max(0, std::min(t, 64) - 1));
+    });
+    return *p[dir];
 }
 
 constexpr size_t SLOT = (size_t)64 << 20;  // bytes per pinned slot
@@ -165,7 +168,7 @@ hipError_t h2d(Staging& sg, void* dev, const void* host, size_t bytes, bool pinn
         const unsigned k = next++ % RING;
         hipError_t e = hipEventSynchronize(sg.in_ev[k]);  // the slot's previous DMA is done
         if (e != hipSuccess) return e;
-        copy_pool().copy(sg.in[k], static_cast<const char*>(host) + off, len);
+        copy_pool(0).copy(sg.in[k], static_cast<const char*>(host) + off, len);
         e = hipMemcpyAsync(static_cast<char*>(dev) + off, sg.in[k], len, hipMemcpyHostToDevice, sg.s_in);
         if (e == hipSuccess) e = hipEventRecord(sg.in_ev[k], sg.s_in);
         if (e != hipSuccess) return e;
@@ -229,7 +232,7 @@ hipError_t d2h(Staging& sg, void* host, const void* dev, size_t bytes, bool pinn
         const unsigned k = done % RING;
         hipError_t e = hipEventSynchronize(sg.out_ev[k]);
         if (e != hipSuccess) return e;
-        copy_pool().copy(static_cast<char*>(host) + off, sg.out[k], len);
+        copy_pool(1).copy(static_cast<char*>(host) + off, sg.out[k], len);
         done++;
     }
     return hipSuccess;
