@@ -178,3 +178,58 @@ def test_native_sharded_commit_rejects_bad_shapes(torch_mod):
     finally:
         comm.close()
         group.close()
+
+
+@pytest.mark.slow
+@pytest.mark.parametrize("world", [4, 8])
+def test_native_sharded_commit_c3_full_size(torch_mod, world):
+    """C3 (2^22 x 256, LDE x4, cap 16) through the native collective at G = 4 (all-gather of
+    coefficients) and G = 8 (sender-side fold + all-to-all), ranks as threads on one card: every
+    rank's LDE slice, leaves and cap equal the one-GPU commit's (itself bit-exact at C2 and
+    property-checked at C3 in test_gpu_fullsize.py), compared on the device."""
+    torch = torch_mod
+    from boojum_amd import commit
+    from boojum_amd.sharded import LocalGroup, native_columns, native_sharded_commit
+    n_cols, log_n, log_lde, cap = 256, 22, 2, 16
+    nl = 1 << (log_n + log_lde)
+    m = nl // world
+    torch.cuda.empty_cache()
+    trace = commit.synthetic_trace(n_cols, log_n)
+    ws = commit.witness_commit(trace, 1 << log_lde, cap)
+    torch.cuda.synchronize()
+    flat = ws.lde.view(n_cols, nl)
+    group = LocalGroup(world)
+    results, errors = [None] * world, []
+
+    def rank_main(P):
+        try:
+            torch.cuda.set_device(0)
+            s = torch.cuda.Stream()
+            with torch.cuda.stream(s):
+                cols = torch.tensor(native_columns(n_cols, world, P), device="cuda")
+                shard = trace.index_select(0, cols).contiguous()
+                comm = group.comm(P)
+                r = native_sharded_commit(comm, shard, n_cols, log_n, log_lde, cap)
+                s.synchronize()
+                del shard
+                results[P] = (bool(torch.equal(r.lde, flat[:, P * m:(P + 1) * m])),
+                              bool(torch.equal(r.leaves, ws.leaves[P * m:(P + 1) * m])),
+                              bool(torch.equal(r.cap, ws.cap)))
+                del r
+                comm.close()
+        except Exception as e:  # noqa: BLE001 - reported below
+            errors.append((P, repr(e)))
+
+    threads = [threading.Thread(target=rank_main, args=(P,), daemon=True) for P in range(world)]
+    for t in threads:
+        t.start()
+    for t in threads:
+        t.join(timeout=240)
+    assert not any(t.is_alive() for t in threads), "a rank did not finish"
+    group.close()
+    assert not errors, errors
+    for P, (lde_ok, leaves_ok, cap_ok) in enumerate(results):
+        assert lde_ok and leaves_ok and cap_ok, "rank %d of %d: lde %s leaves %s cap %s" % (
+            P, world, lde_ok, leaves_ok, cap_ok)
+    del ws, flat, trace
+    torch.cuda.empty_cache()
