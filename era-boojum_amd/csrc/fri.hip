@@ -11,6 +11,7 @@
 // reference loops use. Outputs are canonical.
 #include <hip/hip_runtime.h>
 #include "gl.hpp"
+#include "gl_asm.hpp"
 #include "bj_internal.hpp"
 
 namespace bj {
@@ -18,25 +19,46 @@ namespace bj {
 namespace {
 
 constexpr uint64_t EXT2_NON_RESIDUE = 7;  // GoldilocksExt2::NON_RESIDUE (extension.rs:14-16)
+static_assert(EXT2_NON_RESIDUE == (1u << 3) - 1, "the fold multiplies by the non-residue as 2^3 v - v");
 
-__global__ __launch_bounds__(256) void fri_fold_kernel(const uint64_t* __restrict__ c0, const uint64_t* __restrict__ c1,
-                                                       size_t n_out, const uint64_t* __restrict__ roots,
-                                                       uint64_t coset_inverse, uint64_t ch0, uint64_t ch1,
-                                                       uint64_t* __restrict__ d0, uint64_t* __restrict__ d1) {
+__device__ __forceinline__ void halves(uint64_t x, uint32_t& lo, uint32_t& hi) {
+    lo = (uint32_t)x;
+    hi = (uint32_t)(x >> 32);
+}
+__device__ __forceinline__ uint64_t join(uint32_t lo, uint32_t hi) { return ((uint64_t)hi << 32) | lo; }
+
+// beta = alpha * coset_inverse (an Ext2 times a base element, folded on the host) and
+// bsum = beta0 + beta1, so each output costs six products: (d0, d1) * roots[i] (2), the Karatsuba
+// Ext2 product by beta (3) and the non-residue multiple (1), as interleaved gfx950 asm products
+// (glasm, 14 instructions each).  Pairs (x, -x) are one 16-byte load per column.
+__global__ __launch_bounds__(256) void fri_fold_kernel(const ulonglong2* __restrict__ c0,
+                                                       const ulonglong2* __restrict__ c1, size_t n_out,
+                                                       const uint64_t* __restrict__ roots, uint64_t beta0,
+                                                       uint64_t beta1, uint64_t bsum, uint64_t* __restrict__ d0,
+                                                       uint64_t* __restrict__ d1) {
+    uint32_t b0l, b0h, b1l, b1h, bsl, bsh;
+    halves(beta0, b0l, b0h);
+    halves(beta1, b1l, b1h);
+    halves(bsum, bsl, bsh);
     for (size_t i = blockIdx.x * (size_t)blockDim.x + threadIdx.x; i < n_out; i += (size_t)gridDim.x * blockDim.x) {
-        const uint64_t x0 = c0[2 * i], mx0 = c0[2 * i + 1];
-        const uint64_t x1 = c1[2 * i], mx1 = c1[2 * i + 1];
-        const uint64_t r = gl::mul(roots[i], coset_inverse);
-        const uint64_t a0 = gl::mul(gl::sub(x0, mx0), r);
-        const uint64_t a1 = gl::mul(gl::sub(x1, mx1), r);
-        // (a0 + a1 u) (ch0 + ch1 u), u^2 = 7
-        const uint64_t v0 = gl::mul(a0, ch0);
-        const uint64_t v1 = gl::mul(a1, ch1);
-        const uint64_t m = gl::mul(gl::add(a0, a1), gl::add(ch0, ch1));
-        const uint64_t e1 = gl::sub(gl::sub(m, v0), v1);
-        const uint64_t e0 = gl::add(v0, gl::mul(v1, EXT2_NON_RESIDUE));
-        d0[i] = gl::canon(gl::add(gl::add(e0, x0), mx0));
-        d1[i] = gl::canon(gl::add(gl::add(e1, x1), mx1));
+        const ulonglong2 p0 = c0[i], p1 = c1[i];  // (f(x), f(-x)) of each component
+        const uint64_t r = roots[i];
+        uint32_t s0l, s0h, s1l, s1h, rl, rh;
+        halves(gl::sub(p0.x, p0.y), s0l, s0h);
+        halves(gl::sub(p1.x, p1.y), s1l, s1h);
+        halves(r, rl, rh);
+        uint32_t a0l, a0h, a1l, a1h;
+        glasm::mul_x2(s0l, s0h, rl, rh, a0l, a0h, s1l, s1h, rl, rh, a1l, a1h);
+        uint32_t sal, sah;
+        halves(gl::add(join(a0l, a0h), join(a1l, a1h)), sal, sah);
+        // (a0 + a1 u) (beta0 + beta1 u), u^2 = 7 (field/traits/field.rs:407-424)
+        uint32_t v0l, v0h, v1l, v1h, ml, mh;
+        glasm::mul_x3(a0l, a0h, b0l, b0h, v0l, v0h, a1l, a1h, b1l, b1h, v1l, v1h, sal, sah, bsl, bsh, ml, mh);
+        const uint64_t v0 = join(v0l, v0h), v1 = join(v1l, v1h);
+        const uint64_t e1 = gl::sub(gl::sub(join(ml, mh), v0), v1);
+        const uint64_t e0 = gl::add(v0, gl::sub(gl::mul_pow2_small(v1, 3), v1));  // v0 + 7 v1
+        d0[i] = gl::canon(gl::add(gl::add(e0, p0.x), p0.y));
+        d1[i] = gl::canon(gl::add(gl::add(e1, p1.x), p1.y));
     }
 }
 
@@ -46,10 +68,14 @@ hipError_t launch_fri_fold(const uint64_t* c0, const uint64_t* c1, size_t n_out,
                            uint64_t coset_inverse, uint64_t ch0, uint64_t ch1, uint64_t* d0, uint64_t* d1,
                            hipStream_t st) {
     if (n_out == 0) return hipSuccess;
+    if (((uintptr_t)c0 | (uintptr_t)c1) % 16) return hipErrorInvalidValue;  // pairs are 16-byte loads
     size_t blocks = (n_out + 255) / 256;
     if (blocks > 65536) blocks = 65536;
-    hipLaunchKernelGGL(fri_fold_kernel, dim3((unsigned)blocks), dim3(256), 0, st, c0, c1, n_out, roots,
-                       gl::canon(coset_inverse), gl::canon(ch0), gl::canon(ch1), d0, d1);
+    const uint64_t beta0 = gl::canon(gl::mul(ch0, coset_inverse)), beta1 = gl::canon(gl::mul(ch1, coset_inverse));
+    const uint64_t bsum = gl::canon(gl::add(beta0, beta1));
+    hipLaunchKernelGGL(fri_fold_kernel, dim3((unsigned)blocks), dim3(256), 0, st,
+                       reinterpret_cast<const ulonglong2*>(c0), reinterpret_cast<const ulonglong2*>(c1), n_out, roots,
+                       beta0, beta1, bsum, d0, d1);
     return hipGetLastError();
 }
 

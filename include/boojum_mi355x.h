@@ -330,7 +330,8 @@ int bj_sharded_query_h(bj_comm* comm, const uint64_t* lde, const uint64_t* leave
  *   dst_i = f(x) + f(-x) + alpha * (f(x) - f(-x)) * roots[i] * coset_inverse,  i < n_src / 2,
  * f(x) = (c0[2i], c1[2i]), f(-x) = (c0[2i+1], c1[2i+1]), alpha = (ch0, ch1), u^2 = 7.
  * roots: the INVERSED bit-reversed twiddles of the full FRI domain (bj_precompute_twiddles_d
- * with inverse = 1), indexed by the flat pair index.  Device pointers; outputs canonical. */
+ * with inverse = 1), indexed by the flat pair index.  Device pointers (c0, c1 16-byte aligned:
+ * each (f(x), f(-x)) pair is one load); outputs canonical. */
 int bj_fri_fold_d(const uint64_t* c0, const uint64_t* c1, size_t n_src, const uint64_t* roots,
                   uint64_t coset_inverse, uint64_t ch0, uint64_t ch1, uint64_t* dst_c0, uint64_t* dst_c1,
                   void* stream);
