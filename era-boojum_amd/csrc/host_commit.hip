@@ -8,11 +8,10 @@
 // 16, then 32 columns (multiples of the sponge rate); the leaf sponges carry their capacity words
 // between chunks (bj_merkle_leaves_partial_d), so outputs equal the one-shot commit.
 //
-// Pageable caller memory is staged through a small ring of pinned slots per direction: a pool of
-// host threads copies between the caller's buffer and a slot while the neighbouring slots cross
-// PCIe (copy engine in, CU stores out: see store_to_host).  The runtime's own pageable path halves its rate when both directions run
-// at once (28 GB/s each way against 49 GB/s pinned, tools/duplex_probe.py); the host copies run
-// at 130 GB/s on 8 threads.  Memory the caller has page-locked itself is DMA'd directly.
+// The trace goes in on the copy engine (the runtime's pageable path).  The outputs come back
+// through a small ring of pinned slots: CU store kernels write a slot (store_to_host) while a
+// pool of host threads copies the previous one into the caller's buffer (130 GB/s on 8
+// threads).  Memory the caller has page-locked itself is written directly.
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
@@ -100,30 +99,26 @@ class CopyPool {
     unsigned parts_ = 1;
 };
 
-// One pool per direction (the copy-in and copy-out sides run at once and must not queue behind
-// each other), BJ_COPY_THREADS (default 6) threads each, counting the calling thread.
-CopyPool& copy_pool(int dir) {
-    static CopyPool* p[2] = {nullptr, nullptr};
-    static std::once_flag once;
-    std::call_once(once, [] {
+// BJ_COPY_THREADS (default 6) threads share each copy-out, counting the calling thread.
+CopyPool& copy_pool() {
+    static CopyPool* p = [] {
         const char* e = std::getenv("BJ_COPY_THREADS");
         const int t = e ? std::atoi(e) : 6;
-        for (auto& q : p) q = new CopyPool((unsigned)std::max(0, std::min(t, 64) - 1));
-    });
-    return *p[dir];
+        return new CopyPool((unsigned)std::max(0, std::min(t, 64) - 1));
+    }();
+    return *p;
 }
 
 constexpr size_t SLOT = (size_t)64 << 20;  // bytes per pinned slot
-constexpr int RING = 3;                    // slots per direction
+constexpr int RING = 3;                    // copy-out slots
 
 // Per calling thread and device: pinned slots, their reuse events, and the three streams
 // (created once: stream creation and pinning cost milliseconds).  Calls from one thread are
 // sequential, so reuse is safe.
 struct Staging {
     bool ok = false;
-    char* in[RING] = {};
     char* out[RING] = {};
-    hipEvent_t in_ev[RING] = {}, out_ev[RING] = {};
+    hipEvent_t out_ev[RING] = {};
     hipStream_t s_in = nullptr, s_cmp = nullptr, s_out = nullptr;
 };
 
@@ -134,9 +129,7 @@ int staging(Staging** out) {
     Staging& sg = tl[dev];
     if (!sg.ok) {
         for (int i = 0; i < RING; i++) {
-            HIP_CHECK(hipHostMalloc((void**)&sg.in[i], SLOT, hipHostMallocDefault), "hipHostMalloc");
             HIP_CHECK(hipHostMalloc((void**)&sg.out[i], SLOT, hipHostMallocDefault), "hipHostMalloc");
-            HIP_CHECK(hipEventCreateWithFlags(&sg.in_ev[i], hipEventDisableTiming), "hipEventCreate");
             HIP_CHECK(hipEventCreateWithFlags(&sg.out_ev[i], hipEventDisableTiming), "hipEventCreate");
         }
         HIP_CHECK(hipStreamCreateWithFlags(&sg.s_in, hipStreamNonBlocking), "hipStreamCreate");
@@ -156,24 +149,6 @@ bool is_pinned(const void* p) {
         return false;
     }
     return a.type == hipMemoryTypeHost;
-}
-
-// device <- host over stream s; pageable memory goes through the input slots (host copy of
-// piece i+1 overlaps the DMA of piece i).  Asynchronous once it returns.
-hipError_t h2d(Staging& sg, void* dev, const void* host, size_t bytes, bool pinned) {
-    if (pinned || bytes == 0) return bytes ? hipMemcpyAsync(dev, host, bytes, hipMemcpyHostToDevice, sg.s_in) : hipSuccess;
-    static thread_local unsigned next = 0;
-    for (size_t off = 0; off < bytes; off += SLOT) {
-        const size_t len = std::min(SLOT, bytes - off);
-        const unsigned k = next++ % RING;
-        hipError_t e = hipEventSynchronize(sg.in_ev[k]);  // the slot's previous DMA is done
-        if (e != hipSuccess) return e;
-        copy_pool(0).copy(sg.in[k], static_cast<const char*>(host) + off, len);
-        e = hipMemcpyAsync(static_cast<char*>(dev) + off, sg.in[k], len, hipMemcpyHostToDevice, sg.s_in);
-        if (e == hipSuccess) e = hipEventRecord(sg.in_ev[k], sg.s_in);
-        if (e != hipSuccess) return e;
-    }
-    return hipSuccess;
 }
 
 // Device-to-host copies are CU stores straight into pinned host memory.  The copy engines' own
@@ -232,7 +207,7 @@ hipError_t d2h(Staging& sg, void* host, const void* dev, size_t bytes, bool pinn
         const unsigned k = done % RING;
         hipError_t e = hipEventSynchronize(sg.out_ev[k]);
         if (e != hipSuccess) return e;
-        copy_pool(1).copy(static_cast<char*>(host) + off, sg.out[k], len);
+        copy_pool().copy(static_cast<char*>(host) + off, sg.out[k], len);
         done++;
     }
     return hipSuccess;
@@ -273,7 +248,7 @@ extern "C" int bj_lde_commit_h(const uint64_t* trace_h, uint32_t n_cols, uint32_
         uint64_t keep = UINT64_MAX;
         HIP_CHECK(hipMemPoolSetAttribute(pool, hipMemPoolAttrReleaseThreshold, &keep), "hipMemPoolSetAttribute");
     }
-    const bool pin_tr = n_cols && is_pinned(trace_h), pin_lde = lde_h && is_pinned(lde_h);
+    const bool pin_lde = lde_h && is_pinned(lde_h);
     const size_t tn = n * n_cols;
     uint64_t *tr = nullptr, *mono = nullptr, *lde = nullptr, *lv = nullptr, *nd = nullptr, *st = nullptr;
     HIP_CHECK(hipMallocAsync((void**)&tr, (tn ? tn : 1) * 8, s_cmp), "hipMallocAsync");
@@ -346,7 +321,11 @@ extern "C" int bj_lde_commit_h(const uint64_t* trace_h, uint32_t n_cols, uint32_
     for (uint32_t k = 0; k < n_chunks; k++) {
         const uint32_t c0 = c_first[k], c = c_first[k + 1] - c0;
         const bool last = k + 1 == n_chunks;
-        HIP_CHECK(h2d(sg, tr + (size_t)c0 * n, trace_h + (size_t)c0 * n, (size_t)c * n * 8, pin_tr), "memcpy trace");
+        // host-to-device stays on the copy engine: the runtime's own path for pageable memory
+        // keeps ~56 GB/s here beside the store kernels (staging it through our slots was slower)
+        HIP_CHECK(hipMemcpyAsync(tr + (size_t)c0 * n, trace_h + (size_t)c0 * n, (size_t)c * n * 8,
+                                 hipMemcpyHostToDevice, s_in),
+                  "memcpy trace");
         HIP_CHECK(hipEventRecord(ev_in[k], s_in), "hipEventRecord");
         HIP_CHECK(hipStreamWaitEvent(s_cmp, ev_in[k], 0), "hipStreamWaitEvent");
         if (int r = bj_lde_d(tr + (size_t)c0 * n, c, n, log_n, log_lde, mono + (size_t)c0 * n, lde + (size_t)c0 * nl,
