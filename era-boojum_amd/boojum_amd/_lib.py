@@ -15,6 +15,10 @@ _sz = ctypes.c_size_t
 _int = ctypes.c_int
 _vp = ctypes.c_void_p
 _u64p = ctypes.POINTER(ctypes.c_uint64)
+# bj_exchange_fn (include/boojum_mi355x.h): int (*)(void* user, int kind, const void* send, void* recv,
+# size_t bytes, void* stream)
+EXCHANGE_FN = ctypes.CFUNCTYPE(ctypes.c_int, ctypes.c_void_p, ctypes.c_int, ctypes.c_void_p, ctypes.c_void_p,
+                               ctypes.c_size_t, ctypes.c_void_p)
 
 # name -> argtypes (restype int unless noted).  Every symbol the header declares.
 SIGNATURES = {
@@ -56,19 +60,20 @@ SIGNATURES = {
     "bj_keccak256_leaf_h": ([_u64p, _sz, _u64p], _int),
     "bj_keccak256_node_h": ([_u64p, _u64p, _u64p], _int),
     "bj_blake2s_node_h": ([_u64p, _u64p, _u64p], _int),
-    "bj_lde_commit_d": ([_vp, _u32, _sz, _u32, _u32, _u32, _vp, _vp, _vp, _vp, _u64p, _vp], _int),
-    "bj_lde_commit_h": ([_u64p, _u32, _u32, _u32, _u32, _u64p, _u64p, _u64p, _u64p], _int),
+    "bj_lde_commit_d": ([_vp, _u32, _sz, _u32, _u32, _u32, _u32, _vp, _vp, _vp, _vp, _u64p, _vp], _int),
+    "bj_lde_commit_h": ([_u64p, _u32, _u32, _u32, _u32, _u32, _u64p, _u64p, _u64p, _u64p], _int),
     "bj_comm_rccl_unique_id": ([_vp], _int),
     "bj_comm_init_rccl": ([_vp, _int, _int, ctypes.POINTER(_vp)], _int),
     "bj_comm_wrap_rccl": ([_vp, _int, _int, ctypes.POINTER(_vp)], _int),
     "bj_comm_local_group_create": ([_int, ctypes.POINTER(_vp)], _int),
     "bj_comm_local_group_destroy": ([_vp], _int),
     "bj_comm_init_local": ([_vp, _int, ctypes.POINTER(_vp)], _int),
+    "bj_comm_init_callback": ([_int, _int, EXCHANGE_FN, _vp, _int, ctypes.POINTER(_vp)], _int),
     "bj_comm_destroy": ([_vp], _int),
     "bj_sharded_columns": ([_u32, _u32, _u32, _int, ctypes.POINTER(_u32)], _int),
-    "bj_sharded_commit_d": ([_vp, _vp, _sz, _u32, _u32, _u32, _u32, _int, _vp, _vp, _vp, _vp, _vp], _int),
-    "bj_sharded_query_h": ([_vp, _vp, _vp, _vp, _u32, _u32, _u32, _u32, _int, _u64, _u64p, _u64p, _u64p, _vp],
-                           _int),
+    "bj_sharded_commit_d": ([_vp, _vp, _sz, _u32, _u32, _u32, _u32, _u32, _int, _vp, _vp, _vp, _vp, _vp], _int),
+    "bj_sharded_query_h": ([_vp, _vp, _vp, _vp, _u32, _u32, _u32, _u32, _u32, _int, _u64, _u64p, _u64p, _u64p,
+                            _vp], _int),
     "bj_fri_fold_d": ([_vp, _vp, _sz, _vp, _u64, _u64, _u64, _vp, _vp, _vp], _int),
     "bj_fill_synthetic_d": ([_vp, _u32, _sz, _u32, _u64, _u64, _vp], _int),
     "bj_gl_op_d": ([_int, _vp, _vp, _vp, _sz, _vp], _int),

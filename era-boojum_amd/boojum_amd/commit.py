@@ -1,9 +1,10 @@
 """The witness-commitment hot path as one batched call.
 
-`witness_commit` = prover.rs:313-353 with fri_lde_factor == lde degree: LDE of every
-column (transform_raw_storages_to_lde), MerkleTreeWithCap::construct over the n*D rows,
-get_cap.  `CommitWorkspace` preallocates every HBM buffer once so repeated commits
-(the bench loop, a prover running many circuits) never allocate.
+`witness_commit` = prover.rs:313-353: LDE of every column at D = used_lde_degree
+(transform_raw_storages_to_lde), MerkleTreeWithCap::construct over the rows of the first
+k = fri_lde_factor cosets (subset_for_degree, prover.rs:325-347; k = D unless given), get_cap.
+`CommitWorkspace` preallocates every HBM buffer once so repeated commits (the bench loop, a
+prover running many circuits) never allocate.
 """
 import torch
 
@@ -18,17 +19,22 @@ def _log2(n):
 
 
 class CommitWorkspace:
-    """HBM buffers for a commit of n_cols x 2^log_n at LDE 2^log_lde, cap cap_size.
+    """HBM buffers for a commit of n_cols x 2^log_n at LDE 2^log_lde, tree over the first
+    k = 2^log_commit_cosets cosets (default k = D), cap cap_size.
 
-    Sizes (bytes): scratch 8*C*n, lde 8*C*n*D, leaves 32*n*D, nodes 32*(n*D - cap)."""
+    Sizes (bytes): scratch 8*C*n, lde 8*C*n*D, leaves 32*n*k, nodes 32*(n*k - cap)."""
 
-    def __init__(self, n_cols, log_n, log_lde, cap_size, device="cuda"):
+    def __init__(self, n_cols, log_n, log_lde, cap_size, device="cuda", log_commit_cosets=None):
+        log_k = log_lde if log_commit_cosets is None else log_commit_cosets
+        if not 0 <= log_k <= log_lde:
+            raise ValueError("committed cosets must not exceed the LDE degree")
         n, d = 1 << log_n, 1 << log_lde
-        nl = n * d
+        nl = n << log_k
         _log2(cap_size)
         if nl <= cap_size:
             raise ValueError("tree size must exceed cap size")
         self.n_cols, self.log_n, self.log_lde, self.cap_size = n_cols, log_n, log_lde, cap_size
+        self.log_k = log_k
         self.scratch = torch.empty((n_cols, n), dtype=torch.int64, device=device)
         self.lde = torch.empty((n_cols, d, n), dtype=torch.int64, device=device)
         self.leaves = torch.empty((nl, 4), dtype=torch.int64, device=device)
@@ -44,28 +50,30 @@ class CommitWorkspace:
         return MerkleTreeWithCap(self.cap_size, self.leaves, self.nodes, getattr(self, "hasher", "poseidon2"))
 
 
-def witness_commit(trace, lde_degree, cap_size, workspace=None, hasher="poseidon2"):
-    """Commit a (C, n) int64 CUDA trace tensor.  Returns the workspace holding
-    lde (C, D, n), leaves, nodes and cap (all on device, canonical).
-    Asynchronous on the current stream.  hasher: "poseidon2" (GoldilocksPoseidon2Sponge, the
-    recursive-mode tree), "blake2s" (Blake2s256, the non-recursive one) or "keccak256"."""
+def witness_commit(trace, lde_degree, cap_size, workspace=None, hasher="poseidon2", fri_lde_factor=None):
+    """Commit a (C, n) int64 CUDA trace tensor: LDE at lde_degree (D), tree over the first
+    fri_lde_factor (k, default D) cosets.  Returns the workspace holding lde (C, D, n), leaves
+    (k n, 4), nodes and cap (all on device, canonical).  Asynchronous on the current stream.
+    hasher: "poseidon2" (GoldilocksPoseidon2Sponge, the recursive-mode tree), "blake2s"
+    (Blake2s256, the non-recursive one) or "keccak256"."""
     v, c, n, stride = col_view(trace)
     log_n, log_d = _log2(n), _log2(lde_degree)
-    ws = workspace or CommitWorkspace(c, log_n, log_d, cap_size, device=v.device)
-    if (ws.n_cols, ws.log_n, ws.log_lde, ws.cap_size) != (c, log_n, log_d, cap_size):
+    log_k = log_d if fri_lde_factor is None else _log2(fri_lde_factor)
+    ws = workspace or CommitWorkspace(c, log_n, log_d, cap_size, device=v.device, log_commit_cosets=log_k)
+    if (ws.n_cols, ws.log_n, ws.log_lde, ws.log_k, ws.cap_size) != (c, log_n, log_d, log_k, cap_size):
         raise ValueError("workspace shape does not match the trace")
     st = stream_of(v)
     if hasher == "poseidon2":
-        call("bj_lde_commit_d", v.data_ptr(), c, stride, log_n, log_d, cap_size, ws.scratch.data_ptr(),
+        call("bj_lde_commit_d", v.data_ptr(), c, stride, log_n, log_d, log_k, cap_size, ws.scratch.data_ptr(),
              ws.lde.data_ptr(), ws.leaves.data_ptr(), ws.nodes.data_ptr(), None, st)
     else:
         from .merkle import HASHERS
         if hasher not in HASHERS:
             raise ValueError("unknown tree hasher %r" % (hasher,))
         _, f_leaves, _, f_nodes = HASHERS[hasher]
-        nl = n << log_d
+        nd, nl = n << log_d, n << log_k
         call("bj_lde_d", v.data_ptr(), c, stride, log_n, log_d, ws.scratch.data_ptr(), ws.lde.data_ptr(), st)
-        call(f_leaves, ws.lde.data_ptr(), c, nl, nl, ws.leaves.data_ptr(), st)
+        call(f_leaves, ws.lde.data_ptr(), c, nd, nl, ws.leaves.data_ptr(), st)
         call(f_nodes, ws.leaves.data_ptr(), nl, cap_size, ws.nodes.data_ptr(), st)
     ws.hasher = hasher
     return ws
@@ -124,15 +132,17 @@ class OracleCommitment:
 
 def commit_trace_columns(trace, lde_degree, fri_lde_factor, cap_size, hasher="poseidon2"):
     """Base-field columns (C, n) in Lagrange (trace) form: iFFT, coset LDE at lde_degree, tree
-    over the first fri_lde_factor cosets.  The witness oracle (prover.rs:316-347) and the setup
-    oracle (setup.rs:1146-1204, setup_storage.rs:18-70) are this call."""
-    from .lde import transform_raw_storages_to_lde
+    over the first fri_lde_factor cosets, as one batched commit (bj_lde_commit_d).  The witness
+    oracle (prover.rs:316-347) and the setup oracle (setup.rs:1146-1204, setup_storage.rs:18-70)
+    are this call."""
     from .merkle import MerkleTreeWithCap
     if fri_lde_factor > lde_degree:
         raise ValueError("fri_lde_factor exceeds the LDE degree")
-    lde = transform_raw_storages_to_lde(trace, lde_degree)
-    return OracleCommitment(lde, MerkleTreeWithCap.construct(lde, cap_size, num_cosets=fri_lde_factor,
-                                                             hasher=hasher))
+    t = torch.as_tensor(trace)
+    if not t.is_cuda:
+        t = t.to("cuda")
+    ws = witness_commit(t, lde_degree, cap_size, hasher=hasher, fri_lde_factor=fri_lde_factor)
+    return OracleCommitment(ws.lde, MerkleTreeWithCap(cap_size, ws.leaves, ws.nodes, hasher))
 
 
 def second_stage_commit(z_poly, intermediate_polys, lookup_witness_encoding_polys,

@@ -94,4 +94,10 @@ hipError_t launch_fri_fold(const uint64_t* c0, const uint64_t* c1, size_t n_out,
 namespace bj {
 // capi.hip: set the calling thread's bj_last_error() message; returns code
 int set_error(int code, const char* msg);
+// capi.hip: stream-ordered allocation from the library's private pool of the current device
+// (free with hipFreeAsync); the process's default pool is never reconfigured
+hipError_t pool_alloc(void** p, size_t bytes, hipStream_t st);
+// capi.hip: LDE coset shift 7 * w_{nD}^{bitrev_{log D}(i)} (utils.rs:334-347, 370-373) and the
+// shift of leaf range `shard` of 2^log_shards over the n*D domain, 7 * w_{nD}^{bitrev(shard)}
+uint64_t shard_shift(uint32_t log_n, uint32_t log_lde, uint32_t log_shards, uint32_t shard);
 }  // namespace bj

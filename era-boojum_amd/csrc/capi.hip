@@ -242,12 +242,6 @@ int seam_stream(hipStream_t* out) {
     if (it == tl.end()) {
         hipStream_t st;
         HIP_TRY(hipStreamCreateWithFlags(&st, hipStreamNonBlocking), "hipStreamCreate");
-        // keep the stream-ordered pool's freed memory mapped (as bj_lde_commit_h does), so a
-        // per-column call does not re-map its buffers after every synchronisation
-        hipMemPool_t pool;
-        HIP_TRY(hipDeviceGetDefaultMemPool(&pool, dev), "hipDeviceGetDefaultMemPool");
-        uint64_t keep = UINT64_MAX;
-        HIP_TRY(hipMemPoolSetAttribute(pool, hipMemPoolAttrReleaseThreshold, &keep), "hipMemPoolSetAttribute");
         it = tl.emplace(dev, st).first;
     }
     *out = it->second;
@@ -259,7 +253,7 @@ struct DBuf {
     uint64_t* p = nullptr;
     hipStream_t st = nullptr;
     explicit DBuf(hipStream_t s) : st(s) {}
-    hipError_t alloc(size_t bytes) { return hipMallocAsync((void**)&p, bytes ? bytes : 8, st); }
+    hipError_t alloc(size_t bytes) { return bj::pool_alloc((void**)&p, bytes, st); }
     ~DBuf() { if (p) (void)hipFreeAsync(p, st); }
 };
 
@@ -353,12 +347,49 @@ int shard_from_folded(const uint64_t* folded, size_t folded_stride, uint32_t n_c
 
 namespace bj {
 int set_error(int code, const char* msg) { return fail(code, msg); }
+
+uint64_t shard_shift(uint32_t log_n, uint32_t log_lde, uint32_t log_shards, uint32_t shard) {
+    return ::shard_shift(log_n, log_lde, log_shards, shard);
+}
+
+// The library's own stream-ordered pool per device.  The process's default pool is left
+// alone (its release threshold belongs to the host application); ours keeps freed memory
+// mapped between calls, so a repeated commit does not re-map its workspace after every
+// synchronisation (~20 ms for C2's 5 GB).
+hipError_t pool_alloc(void** p, size_t bytes, hipStream_t st) {
+    static std::mutex mu;
+    static std::map<int, hipMemPool_t>* pools = new std::map<int, hipMemPool_t>();
+    int dev = 0;
+    hipError_t e = hipGetDevice(&dev);
+    if (e != hipSuccess) return e;
+    hipMemPool_t pool = nullptr;
+    {
+        std::lock_guard<std::mutex> lk(mu);
+        auto it = pools->find(dev);
+        if (it == pools->end()) {
+            hipMemPoolProps props;
+            std::memset(&props, 0, sizeof(props));
+            props.allocType = hipMemAllocationTypePinned;
+            props.handleTypes = hipMemHandleTypeNone;
+            props.location.type = hipMemLocationTypeDevice;
+            props.location.id = dev;
+            e = hipMemPoolCreate(&pool, &props);
+            if (e != hipSuccess) return e;
+            uint64_t keep = UINT64_MAX;
+            e = hipMemPoolSetAttribute(pool, hipMemPoolAttrReleaseThreshold, &keep);
+            if (e != hipSuccess) return e;
+            it = pools->emplace(dev, pool).first;
+        }
+        pool = it->second;
+    }
+    return hipMallocFromPoolAsync(p, bytes ? bytes : 8, pool, st);
+}
 }  // namespace bj
 
 extern "C" {
 
 const char* bj_last_error(void) { return g_err.c_str(); }
-uint32_t bj_abi_version(void) { return (1u << 16) | 0u; }
+uint32_t bj_abi_version(void) { return (2u << 16) | 0u; }
 
 int bj_prepare(uint32_t log_n) {
     if (int r = check_log_n(log_n)) return r;
@@ -445,7 +476,7 @@ int bj_ifft_natural_to_natural_d(uint64_t* cols, uint32_t n_cols, size_t col_str
     const size_t n = (size_t)1 << log_n;
     // monomials in bit-reversed order into a temporary, then the bit reversal back in place
     uint64_t* tmp = nullptr;
-    HIP_TRY(hipMallocAsync((void**)&tmp, n * n_cols * 8, S(stream)), "hipMallocAsync");
+    HIP_TRY(bj::pool_alloc((void**)&tmp, n * n_cols * 8, S(stream)), "pool_alloc");
     int r = inverse_to_bitrev(tmp, n, cols, col_stride, n_cols, log_n, S(stream));
     hipError_t e = r == BJ_OK ? bj::launch_bitrev_scale(cols, col_stride, tmp, n, n_cols, log_n, 1, S(stream))
                               : hipSuccess;
@@ -676,13 +707,18 @@ int bj_keccak256_nodes_d(const uint64_t* leaves, size_t n_leaves, uint32_t cap_s
 }
 
 int bj_lde_commit_d(const uint64_t* trace, uint32_t n_cols, size_t trace_stride, uint32_t log_n, uint32_t log_lde,
-                    uint32_t cap_size, uint64_t* scratch, uint64_t* lde, uint64_t* leaves, uint64_t* nodes,
-                    uint64_t* cap_h, void* stream) {
-    const size_t nl = (size_t)1 << (log_n + log_lde);
+                    uint32_t log_commit_cosets, uint32_t cap_size, uint64_t* scratch, uint64_t* lde, uint64_t* leaves,
+                    uint64_t* nodes, uint64_t* cap_h, void* stream) {
+    if (log_commit_cosets > log_lde)
+        return fail(BJ_EINVAL, "committed cosets exceed the lde degree (prover.rs:313, lde.rs:298-308)");
+    // the tree covers the first k = 2^log_commit_cosets cosets of every column
+    // (subset_for_degree, lde.rs:298-308): leaf L < k * n of column c is lde[c * D * n + L]
+    const size_t nd = (size_t)1 << (log_n + log_lde);
+    const size_t nl = (size_t)1 << (log_n + log_commit_cosets);
     if (!is_pow2(cap_size) || nl <= cap_size)
-        return fail(BJ_EINVAL, "need power-of-two cap_size < n * D (merkle_tree.rs:83-96)");
+        return fail(BJ_EINVAL, "need power-of-two cap_size < n * k (merkle_tree.rs:83-96)");
     if (int r = bj_lde_d(trace, n_cols, trace_stride, log_n, log_lde, scratch, lde, stream)) return r;
-    if (int r = bj_merkle_leaves_d(lde, n_cols, nl, nl, leaves, stream)) return r;
+    if (int r = bj_merkle_leaves_d(lde, n_cols, nd, nl, leaves, stream)) return r;
     if (int r = bj_merkle_nodes_d(leaves, nl, cap_size, nodes, stream)) return r;
     if (cap_h) {
         HIP_TRY(hipMemcpyAsync(cap_h, nodes + 4 * (nl - 2 * (size_t)cap_size), (size_t)cap_size * 32,

@@ -29,6 +29,7 @@
 
 #include "../../include/boojum_mi355x.h"
 #include "bj_internal.hpp"
+#include "gl.hpp"
 
 namespace {
 
@@ -111,29 +112,41 @@ struct LocalGroup {
     std::condition_variable cv;
     int arrived = 0;
     uint64_t generation = 0;
+    bool aborted = false;  // a rank failed mid-collective: the group is unusable from then on
     std::vector<const void*> slot;
     std::vector<hipEvent_t> ready, done;
 
-    void barrier() {
+    // false when a peer aborted (instead of waiting for it forever)
+    bool barrier() {
         std::unique_lock<std::mutex> lk(mu);
+        if (aborted) return false;
         const uint64_t g = generation;
         if (++arrived == world) {
             arrived = 0;
             generation++;
             cv.notify_all();
-        } else {
-            cv.wait(lk, [&] { return generation != g; });
+            return true;
         }
+        cv.wait(lk, [&] { return generation != g || aborted; });
+        return generation != g;
+    }
+    void abort() {
+        std::lock_guard<std::mutex> lk(mu);
+        aborted = true;
+        cv.notify_all();
     }
 };
 
 }  // namespace
 
 struct bj_comm {
-    enum Kind { RCCL_OWNED, RCCL_WRAPPED, LOCAL } kind;
+    enum Kind { RCCL_OWNED, RCCL_WRAPPED, LOCAL, CALLBACK } kind;
     int world = 1, rank = 0;
     ncclComm_t nccl = nullptr;
     LocalGroup* group = nullptr;
+    bj_exchange_fn fn = nullptr;  // CALLBACK: the caller's exchange
+    void* user = nullptr;
+    int host_staged = 1;
     hipStream_t xs = nullptr;  // exchange stream, high priority, created on first use
     int xs_dev = -1;
 };
@@ -160,7 +173,8 @@ int local_exchange(bj_comm* c, const void* send, void* recv, size_t bytes, bool 
     const int me = c->rank;
     HIP_CHECK(hipEventRecord(g.ready[me], st), "hipEventRecord");
     g.slot[me] = send;
-    g.barrier();  // every rank's send buffer and ready event are published
+    // every rank's send buffer and ready event are published
+    if (!g.barrier()) return err(BJ_EINVAL, "a peer rank of the local group failed");
     for (int p = 0; p < g.world; p++) {
         HIP_CHECK(hipStreamWaitEvent(st, g.ready[p], 0), "hipStreamWaitEvent");
         const char* src = static_cast<const char*>(g.slot[p]) + (all_to_all ? (size_t)me * bytes : 0);
@@ -168,9 +182,34 @@ int local_exchange(bj_comm* c, const void* send, void* recv, size_t bytes, bool 
         if (src != dst && bytes) HIP_CHECK(hipMemcpyAsync(dst, src, bytes, hipMemcpyDeviceToDevice, st), "memcpy");
     }
     HIP_CHECK(hipEventRecord(g.done[me], st), "hipEventRecord");
-    g.barrier();  // every rank has queued its reads of the others' buffers
+    // every rank has queued its reads of the others' buffers
+    if (!g.barrier()) return err(BJ_EINVAL, "a peer rank of the local group failed");
     for (int p = 0; p < g.world; p++) HIP_CHECK(hipStreamWaitEvent(st, g.done[p], 0), "hipStreamWaitEvent");
-    g.barrier();  // nobody re-records this round's events before all waits are queued
+    // nobody re-records this round's events before all waits are queued
+    if (!g.barrier()) return err(BJ_EINVAL, "a peer rank of the local group failed");
+    return BJ_OK;
+}
+
+// The caller's exchange (bj_comm_init_callback).  Host-staged: the device data goes to host
+// memory, the callback exchanges host buffers (gloo, MPI, ...), the result comes back; every
+// step synchronises, so this transport is for rehearsal and tests, not for overlap.  Device
+// mode hands the callback device pointers and the stream to order its work on.
+int callback_exchange(bj_comm* c, int kind, const void* send, void* recv, size_t bytes, hipStream_t st) {
+    const size_t world = (size_t)c->world;
+    const size_t send_bytes = kind == BJ_XCHG_ALL_TO_ALL ? world * bytes : bytes, recv_bytes = world * bytes;
+    if (!c->host_staged) {
+        if (int r = c->fn(c->user, kind, send, recv, bytes, st))
+            return err(BJ_EINVAL, "exchange callback failed (" + std::to_string(r) + ")");
+        return BJ_OK;
+    }
+    std::vector<uint8_t> hs(send_bytes), hr(recv_bytes);
+    HIP_CHECK(hipStreamSynchronize(st), "sync");
+    if (send_bytes) HIP_CHECK(hipMemcpyAsync(hs.data(), send, send_bytes, hipMemcpyDeviceToHost, st), "memcpy");
+    HIP_CHECK(hipStreamSynchronize(st), "sync");
+    if (int r = c->fn(c->user, kind, hs.data(), hr.data(), bytes, nullptr))
+        return err(BJ_EINVAL, "exchange callback failed (" + std::to_string(r) + ")");
+    if (recv_bytes) HIP_CHECK(hipMemcpyAsync(recv, hr.data(), recv_bytes, hipMemcpyHostToDevice, st), "memcpy");
+    HIP_CHECK(hipStreamSynchronize(st), "sync");
     return BJ_OK;
 }
 
@@ -181,6 +220,7 @@ int all_gather(bj_comm* c, const void* send, void* recv, size_t bytes, hipStream
         return BJ_OK;
     }
     if (c->kind == bj_comm::LOCAL) return local_exchange(c, send, recv, bytes, false, st);
+    if (c->kind == bj_comm::CALLBACK) return callback_exchange(c, BJ_XCHG_ALL_GATHER, send, recv, bytes, st);
     const Rccl& R = rccl();
     RCCL_CHECK(R, R.all_gather(send, recv, bytes / 8, ncclUint64, c->nccl, st), "ncclAllGather");
     return BJ_OK;
@@ -193,6 +233,7 @@ int all_to_all(bj_comm* c, const void* send, void* recv, size_t bytes, hipStream
         return BJ_OK;
     }
     if (c->kind == bj_comm::LOCAL) return local_exchange(c, send, recv, bytes, true, st);
+    if (c->kind == bj_comm::CALLBACK) return callback_exchange(c, BJ_XCHG_ALL_TO_ALL, send, recv, bytes, st);
     const Rccl& R = rccl();
     RCCL_CHECK(R, R.group_start(), "ncclGroupStart");
     for (int p = 0; p < c->world; p++) {
@@ -255,7 +296,7 @@ struct Workspace {
     std::vector<void*> ptrs;
     explicit Workspace(hipStream_t s) : st(s) {}
     hipError_t alloc(uint64_t** p, size_t elems) {
-        hipError_t e = hipMallocAsync(reinterpret_cast<void**>(p), std::max<size_t>(elems, 1) * 8, st);
+        hipError_t e = bj::pool_alloc(reinterpret_cast<void**>(p), elems * 8, st);
         if (e == hipSuccess) ptrs.push_back(*p);
         return e;
     }
@@ -277,6 +318,35 @@ struct Events {
     }
     ~Events() {
         for (hipEvent_t e : ev) (void)hipEventDestroy(e);
+    }
+};
+
+// Error paths of a collective.  GroupAbort (armed from the first line): unless the call
+// completes, an in-process group is aborted so its peers fail instead of blocking in a barrier
+// (a rank that rejects its arguments aborts them too).  XsJoin (declared after the workspace,
+// so it runs before the workspace frees on the compute stream): unless the call completes, the
+// compute stream first waits for everything already queued on the exchange stream.
+struct GroupAbort {
+    bj_comm* c;
+    bool ok = false;
+    explicit GroupAbort(bj_comm* c_) : c(c_) {}
+    ~GroupAbort() {
+        if (!ok && c && c->kind == bj_comm::LOCAL) c->group->abort();
+    }
+};
+struct XsJoin {
+    hipStream_t st, xs;
+    bool ok = false;
+    XsJoin(hipStream_t st_, hipStream_t xs_) : st(st_), xs(xs_) {}
+    ~XsJoin() {
+        if (ok || !xs) return;
+        hipEvent_t e;
+        if (hipEventCreateWithFlags(&e, hipEventDisableTiming) == hipSuccess) {
+            if (hipEventRecord(e, xs) == hipSuccess) (void)hipStreamWaitEvent(st, e, 0);
+            (void)hipEventDestroy(e);
+        } else {
+            (void)hipStreamSynchronize(xs);
+        }
     }
 };
 
@@ -380,6 +450,21 @@ int bj_comm_init_local(void* group, int rank, bj_comm** out) {
     return BJ_OK;
 }
 
+int bj_comm_init_callback(int world, int rank, bj_exchange_fn fn, void* user, int host_staged, bj_comm** out) {
+    if (!fn || !out) return err(BJ_EINVAL, "null argument");
+    if (world < 1 || !is_pow2((uint64_t)world) || rank < 0 || rank >= world)
+        return err(BJ_EINVAL, "world must be a power of two and 0 <= rank < world");
+    bj_comm* c = new bj_comm();
+    c->kind = bj_comm::CALLBACK;
+    c->world = world;
+    c->rank = rank;
+    c->fn = fn;
+    c->user = user;
+    c->host_staged = host_staged ? 1 : 0;
+    *out = c;
+    return BJ_OK;
+}
+
 int bj_comm_destroy(bj_comm* c) {
     if (!c) return BJ_OK;
     int rc = BJ_OK;
@@ -406,18 +491,25 @@ int bj_sharded_columns(uint32_t n_cols, uint32_t log_shards, uint32_t shard, int
 }
 
 int bj_sharded_commit_d(bj_comm* comm, const uint64_t* trace_shard, size_t trace_stride, uint32_t n_cols,
-                        uint32_t log_n, uint32_t log_lde, uint32_t cap_size, int hasher, uint64_t* lde,
-                        uint64_t* leaves, uint64_t* nodes, uint64_t* cap, void* stream) {
+                        uint32_t log_n, uint32_t log_lde, uint32_t log_commit_cosets, uint32_t cap_size, int hasher,
+                        uint64_t* lde, uint64_t* leaves, uint64_t* nodes, uint64_t* cap, void* stream) {
     if (!comm) return err(BJ_EINVAL, "null communicator");
+    GroupAbort abort_guard(comm);
     if (hasher < BJ_HASHER_POSEIDON2 || hasher > BJ_HASHER_KECCAK256) return err(BJ_EINVAL, "unknown hasher");
     const uint32_t world = (uint32_t)comm->world, rank = (uint32_t)comm->rank;
-    const uint32_t log_g = log2u(world);
+    const uint32_t log_g = log2u(world), log_k = log_commit_cosets;
     if (n_cols == 0 || n_cols % world) return err(BJ_EINVAL, "n_cols must be a positive multiple of the world size");
     if (log_lde == 0) return err(BJ_EINVAL, "lde degree must be > 1 (utils.rs:283)");
-    if (log_n > 30 || log_g > log_n + log_lde) return err(BJ_EINVAL, "more shards than leaves");
-    const size_t n = (size_t)1 << log_n, nl = n << log_lde, m = nl >> log_g;
-    if (!is_pow2(cap_size) || nl <= cap_size)
-        return err(BJ_EINVAL, "need power-of-two cap_size < n * D (merkle_tree.rs:83-96)");
+    if (log_k > log_lde) return err(BJ_EINVAL, "committed cosets exceed the lde degree (prover.rs:313, lde.rs:298-308)");
+    if (log_n > 30 || log_g > log_n + log_k) return err(BJ_EINVAL, "more shards than committed leaves");
+    if (log_g > log_k && log_g - log_k > 6) return err(BJ_EINVAL, "G / k exceeds 64");
+    // m: this rank's leaves (and its share of each k-coset block of the LDE); B blocks of k cosets
+    const size_t n = (size_t)1 << log_n, nk = n << log_k, m = nk >> log_g;
+    const uint32_t B = 1u << (log_lde - log_k);
+    // rank P's part of block j is leaf range j * G + P of the D-coset domain cut into 2^ls ranges
+    const uint32_t ls = log_g + log_lde - log_k;
+    if (!is_pow2(cap_size) || nk <= cap_size)
+        return err(BJ_EINVAL, "need power-of-two cap_size < n * k (merkle_tree.rs:83-96)");
     const uint32_t cap_local = std::max<uint32_t>(1, cap_size / world);
     if (m <= cap_local) return err(BJ_EINVAL, "each shard needs more leaves than its cap slice");
     if (trace_stride < n) return err(BJ_EINVAL, "trace_stride < n");
@@ -427,44 +519,59 @@ int bj_sharded_commit_d(bj_comm* comm, const uint64_t* trace_shard, size_t trace
     hipStream_t xs = nullptr;
     if (world > 1) BJ_CHECK(exchange_stream(comm, &xs));
     const uint32_t cpr = n_cols / world;
+    // G > D: the sender folds (m < n values per column and block); else all-gather n per column
     const bool fold = log_g > log_lde;
+    const uint32_t log_f = ls > log_lde ? ls - log_lde : 0;  // folding factor per transform
     const std::vector<Run> runs = column_runs(n_cols, world, rank, hasher);
     const size_t K = runs.size();
+    uint32_t max_cc = 0;
+    for (const Run& r : runs) max_cc = std::max(max_cc, r.c1 - r.c0);
 
     Workspace ws(st);
-    uint64_t *coeffs = nullptr, *own = nullptr, *send = nullptr, *folded = nullptr, *state = nullptr;
+    XsJoin xs_join(st, xs);
+    uint64_t *coeffs = nullptr, *own = nullptr, *send = nullptr, *folded = nullptr, *state = nullptr, *work = nullptr;
     if (fold) {
-        HIP_CHECK(ws.alloc(&own, (size_t)cpr * n), "hipMallocAsync");
-        HIP_CHECK(ws.alloc(&send, (size_t)cpr * world * m), "hipMallocAsync");
-        HIP_CHECK(ws.alloc(&folded, (size_t)n_cols * m), "hipMallocAsync");
+        HIP_CHECK(ws.alloc(&own, (size_t)cpr * n), "pool_alloc");
+        HIP_CHECK(ws.alloc(&send, (size_t)cpr * world * B * m), "pool_alloc");
+        HIP_CHECK(ws.alloc(&folded, (size_t)B * n_cols * m), "pool_alloc");
     } else {
-        HIP_CHECK(ws.alloc(&coeffs, (size_t)n_cols * n), "hipMallocAsync");
+        HIP_CHECK(ws.alloc(&coeffs, (size_t)n_cols * n), "pool_alloc");
+        if (log_f) HIP_CHECK(ws.alloc(&work, (size_t)max_cc * m), "pool_alloc");
     }
-    if (K > 1) HIP_CHECK(ws.alloc(&state, m * 4), "hipMallocAsync");
+    if (K > 1) HIP_CHECK(ws.alloc(&state, m * 4), "pool_alloc");
     Events in, arrived;
     if (world > 1) {
         HIP_CHECK(in.make(K), "hipEventCreate");
         HIP_CHECK(arrived.make(K), "hipEventCreate");
     }
+    std::vector<uint64_t> spm(world);
 
     // 1. local inverse transforms (and folds), each chunk's exchange issued as soon as its
     //    part is ready
     for (size_t k = 0; k < K; k++) {
         const Run& r = runs[k];
         const uint64_t* tr = trace_shard + (size_t)r.lo * trace_stride;
+        hipStream_t xst = world > 1 ? xs : st;
         if (fold) {
-            uint64_t* snd = send + (size_t)world * m * r.lo;
-            BJ_CHECK(bj_lde_coeffs_d(tr, r.count, trace_stride, log_n, own + (size_t)r.lo * n, n, st));
-            BJ_CHECK(bj_lde_fold_shards_d(own + (size_t)r.lo * n, r.count, n, log_n, log_lde, log_g, snd,
-                                          (size_t)r.count * m, st));
+            // send layout per run: [block j][rank p][c][m], so block j's all-to-all is contiguous
+            uint64_t* snd = send + (size_t)world * B * m * r.lo;
+            uint64_t* mine = own + (size_t)r.lo * n;
+            BJ_CHECK(bj_lde_coeffs_d(tr, r.count, trace_stride, log_n, mine, n, st));
+            for (uint32_t j = 0; j < B; j++) {
+                for (uint32_t p = 0; p < world; p++)
+                    spm[p] = gl::pow(bj::shard_shift(log_n, log_lde, ls, j * world + p), m);
+                HIP_CHECK(bj::launch_fold_all(snd + (size_t)j * world * r.count * m, m, (size_t)r.count * m, mine, n,
+                                              r.count, log2u(m), log_f, world, spm.data(), st),
+                          "fold");
+            }
             if (world > 1) {
                 HIP_CHECK(hipEventRecord(in.ev[k], st), "hipEventRecord");
                 HIP_CHECK(hipStreamWaitEvent(xs, in.ev[k], 0), "hipStreamWaitEvent");
-                BJ_CHECK(all_to_all(comm, snd, folded + (size_t)r.c0 * m, (size_t)r.count * m * 8, xs));
-                HIP_CHECK(hipEventRecord(arrived.ev[k], xs), "hipEventRecord");
-            } else {
-                BJ_CHECK(all_to_all(comm, snd, folded + (size_t)r.c0 * m, (size_t)r.count * m * 8, st));
             }
+            for (uint32_t j = 0; j < B; j++)
+                BJ_CHECK(all_to_all(comm, snd + (size_t)j * world * r.count * m,
+                                    folded + ((size_t)j * n_cols + r.c0) * m, (size_t)r.count * m * 8, xst));
+            if (world > 1) HIP_CHECK(hipEventRecord(arrived.ev[k], xs), "hipEventRecord");
         } else {
             uint64_t* mine = coeffs + (size_t)r.global * n;
             BJ_CHECK(bj_lde_coeffs_d(tr, r.count, trace_stride, log_n, mine, n, st));
@@ -476,25 +583,31 @@ int bj_sharded_commit_d(bj_comm* comm, const uint64_t* trace_shard, size_t trace
             }
         }
     }
-    // 2. per arrived chunk: this rank's leaf range of its columns' LDE, absorbed into the sponges
+    // 2. per arrived chunk: this rank's part of the committed block (block 0) of its columns'
+    //    LDE, absorbed into the sponges, then its part of the other blocks (LDE only)
     for (size_t k = 0; k < K; k++) {
         const Run& r = runs[k];
         const uint32_t cc = r.c1 - r.c0;
-        uint64_t* out = lde + (size_t)r.c0 * m;
         if (world > 1) HIP_CHECK(hipStreamWaitEvent(st, arrived.ev[k], 0), "hipStreamWaitEvent");
-        if (fold)
-            BJ_CHECK(bj_lde_shard_folded_d(folded + (size_t)r.c0 * m, cc, m, log_n, log_lde, log_g, rank, out, st));
-        else
-            BJ_CHECK(bj_lde_shard_d(coeffs + (size_t)r.c0 * n, cc, n, log_n, log_lde, log_g, rank, nullptr, out, st));
-        const bool last = k + 1 == K;
-        const uint64_t* cin = k == 0 ? nullptr : state;
-        uint64_t* dst = last ? leaves : state;
-        if (hasher == BJ_HASHER_POSEIDON2)
-            BJ_CHECK(bj_merkle_leaves_partial_d(out, cc, m, m, cin, dst, last ? 1 : 0, st));
-        else if (hasher == BJ_HASHER_BLAKE2S)
-            BJ_CHECK(bj_blake2s_leaves_partial_d(out, cc, m, m, r.c0, cin, dst, last ? 1 : 0, st));
-        else
-            BJ_CHECK(bj_keccak256_leaves_d(out, cc, m, m, dst, st));
+        for (uint32_t j = 0; j < B; j++) {
+            uint64_t* out = lde + ((size_t)j * n_cols + r.c0) * m;
+            const uint32_t shard = j * world + rank;
+            if (fold)
+                BJ_CHECK(bj_lde_shard_folded_d(folded + ((size_t)j * n_cols + r.c0) * m, cc, m, log_n, log_lde, ls,
+                                               shard, out, st));
+            else
+                BJ_CHECK(bj_lde_shard_d(coeffs + (size_t)r.c0 * n, cc, n, log_n, log_lde, ls, shard, work, out, st));
+            if (j) continue;
+            const bool last = k + 1 == K;
+            const uint64_t* cin = k == 0 ? nullptr : state;
+            uint64_t* dst = last ? leaves : state;
+            if (hasher == BJ_HASHER_POSEIDON2)
+                BJ_CHECK(bj_merkle_leaves_partial_d(out, cc, m, m, cin, dst, last ? 1 : 0, st));
+            else if (hasher == BJ_HASHER_BLAKE2S)
+                BJ_CHECK(bj_blake2s_leaves_partial_d(out, cc, m, m, r.c0, cin, dst, last ? 1 : 0, st));
+            else
+                BJ_CHECK(bj_keccak256_leaves_d(out, cc, m, m, dst, st));
+        }
     }
     // 3. this rank's subtree, then the cap
     BJ_CHECK(nodes_for(hasher, leaves, m, cap_local, nodes, st));
@@ -504,27 +617,32 @@ int bj_sharded_commit_d(bj_comm* comm, const uint64_t* trace_shard, size_t trace
     } else {
         // fewer cap digests than ranks: gather the subtree roots, hash the top levels everywhere
         uint64_t *roots = nullptr, *top = nullptr;
-        HIP_CHECK(ws.alloc(&roots, (size_t)world * 4), "hipMallocAsync");
-        HIP_CHECK(ws.alloc(&top, (size_t)(world - cap_size) * 4), "hipMallocAsync");
+        HIP_CHECK(ws.alloc(&roots, (size_t)world * 4), "pool_alloc");
+        HIP_CHECK(ws.alloc(&top, (size_t)(world - cap_size) * 4), "pool_alloc");
         BJ_CHECK(all_gather(comm, local_cap, roots, 32, st));
         BJ_CHECK(nodes_for(hasher, roots, world, cap_size, top, st));
         HIP_CHECK(hipMemcpyAsync(cap, top + (size_t)(world - 2 * cap_size) * 4, (size_t)cap_size * 32,
                                  hipMemcpyDeviceToDevice, st),
                   "memcpy cap");
     }
+    xs_join.ok = abort_guard.ok = true;
     return BJ_OK;
 }
 
 int bj_sharded_query_h(bj_comm* comm, const uint64_t* lde, const uint64_t* leaves, const uint64_t* nodes,
-                       uint32_t n_cols, uint32_t log_n, uint32_t log_lde, uint32_t cap_size, int hasher, uint64_t idx,
-                       uint64_t* leaf_elements_h, uint64_t* leaf_hash_h, uint64_t* proof_h, void* stream) {
+                       uint32_t n_cols, uint32_t log_n, uint32_t log_lde, uint32_t log_commit_cosets, uint32_t cap_size,
+                       int hasher, uint64_t idx, uint64_t* leaf_elements_h, uint64_t* leaf_hash_h, uint64_t* proof_h,
+                       void* stream) {
     if (!comm) return err(BJ_EINVAL, "null communicator");
+    GroupAbort abort_guard(comm);
     if (hasher < BJ_HASHER_POSEIDON2 || hasher > BJ_HASHER_KECCAK256) return err(BJ_EINVAL, "unknown hasher");
     const uint32_t world = (uint32_t)comm->world, rank = (uint32_t)comm->rank;
     const uint32_t log_g = log2u(world);
-    if (log_n > 30 || log_g > log_n + log_lde || n_cols == 0) return err(BJ_EINVAL, "bad geometry");
-    const size_t nl = (size_t)1 << (log_n + log_lde), m = nl >> log_g;
-    if (!is_pow2(cap_size) || nl <= cap_size) return err(BJ_EINVAL, "need power-of-two cap_size < n * D");
+    if (log_commit_cosets > log_lde) return err(BJ_EINVAL, "committed cosets exceed the lde degree");
+    if (log_n > 30 || log_g > log_n + log_commit_cosets || n_cols == 0) return err(BJ_EINVAL, "bad geometry");
+    // the tree is over the first k cosets; this rank's block-0 slice (its leaves) is lde[c * m + i]
+    const size_t nl = (size_t)1 << (log_n + log_commit_cosets), m = nl >> log_g;
+    if (!is_pow2(cap_size) || nl <= cap_size) return err(BJ_EINVAL, "need power-of-two cap_size < n * k");
     const uint32_t cap_local = std::max<uint32_t>(1, cap_size / world);
     if (m <= cap_local) return err(BJ_EINVAL, "each shard needs more leaves than its cap slice");
     if (idx >= nl) return err(BJ_EINVAL, "tree index out of range");
@@ -537,8 +655,8 @@ int bj_sharded_query_h(bj_comm* comm, const uint64_t* lde, const uint64_t* leave
     const size_t words = (size_t)n_cols + 4 + 4 * ((size_t)local_depth + top_depth);
     Workspace ws(st);
     uint64_t *buf = nullptr, *all = nullptr;
-    HIP_CHECK(ws.alloc(&buf, words), "hipMallocAsync");
-    HIP_CHECK(ws.alloc(&all, words * world), "hipMallocAsync");
+    HIP_CHECK(ws.alloc(&buf, words), "pool_alloc");
+    HIP_CHECK(ws.alloc(&all, words * world), "pool_alloc");
     HIP_CHECK(hipMemsetAsync(buf, 0, words * 8, st), "memset");
     if (rank == owner) {
         // leaf_elements: every column's LDE value at the row (a strided gather), then the leaf
@@ -558,8 +676,8 @@ int bj_sharded_query_h(bj_comm* comm, const uint64_t* lde, const uint64_t* leave
     if (top_depth) {
         // cap < G: the top levels over the G subtree roots, hashed on every rank
         uint64_t *roots = nullptr, *top = nullptr;
-        HIP_CHECK(ws.alloc(&roots, (size_t)world * 4), "hipMallocAsync");
-        HIP_CHECK(ws.alloc(&top, (size_t)(world - cap_size) * 4), "hipMallocAsync");
+        HIP_CHECK(ws.alloc(&roots, (size_t)world * 4), "pool_alloc");
+        HIP_CHECK(ws.alloc(&top, (size_t)(world - cap_size) * 4), "pool_alloc");
         BJ_CHECK(all_gather(comm, nodes + (m - 2 * (size_t)cap_local) * 4, roots, 32, st));
         BJ_CHECK(nodes_for(hasher, roots, world, cap_size, top, st));
         size_t at = owner, level_off = 0, level_len = world;
@@ -582,6 +700,7 @@ int bj_sharded_query_h(bj_comm* comm, const uint64_t* lde, const uint64_t* leave
                              st),
               "memcpy");
     HIP_CHECK(hipStreamSynchronize(st), "sync");
+    abort_guard.ok = true;
     return BJ_OK;
 }
 

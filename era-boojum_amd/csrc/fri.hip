@@ -30,9 +30,17 @@ __device__ __forceinline__ uint64_t join(uint32_t lo, uint32_t hi) { return ((ui
 // beta = alpha * coset_inverse (an Ext2 times a base element, folded on the host) and
 // bsum = beta0 + beta1, so each output costs six products: (d0, d1) * roots[i] (2), the Karatsuba
 // Ext2 product by beta (3) and the non-residue multiple (1), as interleaved gfx950 asm products
-// (glasm, 14 instructions each).  Pairs (x, -x) are one 16-byte load per column.
-__global__ __launch_bounds__(256) void fri_fold_kernel(const ulonglong2* __restrict__ c0,
-                                                       const ulonglong2* __restrict__ c1, size_t n_out,
+// (glasm, 14 instructions each).  Pairs (x, -x) are one 16-byte load per column when both
+// columns are 16-byte aligned (V16), two 8-byte loads otherwise.
+template <bool V16>
+__device__ __forceinline__ ulonglong2 load_pair(const uint64_t* __restrict__ c, size_t i) {
+    if constexpr (V16) return reinterpret_cast<const ulonglong2*>(c)[i];
+    return make_ulonglong2(c[2 * i], c[2 * i + 1]);
+}
+
+template <bool V16>
+__global__ __launch_bounds__(256) void fri_fold_kernel(const uint64_t* __restrict__ c0,
+                                                       const uint64_t* __restrict__ c1, size_t n_out,
                                                        const uint64_t* __restrict__ roots, uint64_t beta0,
                                                        uint64_t beta1, uint64_t bsum, uint64_t* __restrict__ d0,
                                                        uint64_t* __restrict__ d1) {
@@ -41,7 +49,7 @@ __global__ __launch_bounds__(256) void fri_fold_kernel(const ulonglong2* __restr
     halves(beta1, b1l, b1h);
     halves(bsum, bsl, bsh);
     for (size_t i = blockIdx.x * (size_t)blockDim.x + threadIdx.x; i < n_out; i += (size_t)gridDim.x * blockDim.x) {
-        const ulonglong2 p0 = c0[i], p1 = c1[i];  // (f(x), f(-x)) of each component
+        const ulonglong2 p0 = load_pair<V16>(c0, i), p1 = load_pair<V16>(c1, i);  // (f(x), f(-x))
         const uint64_t r = roots[i];
         uint32_t s0l, s0h, s1l, s1h, rl, rh;
         halves(gl::sub(p0.x, p0.y), s0l, s0h);
@@ -68,14 +76,17 @@ hipError_t launch_fri_fold(const uint64_t* c0, const uint64_t* c1, size_t n_out,
                            uint64_t coset_inverse, uint64_t ch0, uint64_t ch1, uint64_t* d0, uint64_t* d1,
                            hipStream_t st) {
     if (n_out == 0) return hipSuccess;
-    if (((uintptr_t)c0 | (uintptr_t)c1) % 16) return hipErrorInvalidValue;  // pairs are 16-byte loads
+    if (((uintptr_t)c0 | (uintptr_t)c1) % 8) return hipErrorInvalidValue;  // u64 elements
     size_t blocks = (n_out + 255) / 256;
     if (blocks > 65536) blocks = 65536;
     const uint64_t beta0 = gl::canon(gl::mul(ch0, coset_inverse)), beta1 = gl::canon(gl::mul(ch1, coset_inverse));
     const uint64_t bsum = gl::canon(gl::add(beta0, beta1));
-    hipLaunchKernelGGL(fri_fold_kernel, dim3((unsigned)blocks), dim3(256), 0, st,
-                       reinterpret_cast<const ulonglong2*>(c0), reinterpret_cast<const ulonglong2*>(c1), n_out, roots,
-                       beta0, beta1, bsum, d0, d1);
+    if (((uintptr_t)c0 | (uintptr_t)c1) % 16 == 0)
+        hipLaunchKernelGGL(fri_fold_kernel<true>, dim3((unsigned)blocks), dim3(256), 0, st, c0, c1, n_out, roots,
+                           beta0, beta1, bsum, d0, d1);
+    else
+        hipLaunchKernelGGL(fri_fold_kernel<false>, dim3((unsigned)blocks), dim3(256), 0, st, c0, c1, n_out, roots,
+                           beta0, beta1, bsum, d0, d1);
     return hipGetLastError();
 }
 

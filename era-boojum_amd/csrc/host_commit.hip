@@ -112,34 +112,91 @@ CopyPool& copy_pool() {
 constexpr size_t SLOT = (size_t)64 << 20;  // bytes per pinned slot
 constexpr int RING = 3;                    // copy-out slots
 
-// Per calling thread and device: pinned slots, their reuse events, and the three streams
-// (created once: stream creation and pinning cost milliseconds).  Calls from one thread are
-// sequential, so reuse is safe.
+// A staging set: pinned slots, their reuse events, and the three streams (created once:
+// stream creation and pinning cost milliseconds).  The sets live in a bounded per-device pool
+// shared by every calling thread: a call takes a free set (or makes one while fewer than
+// kMaxStaging exist, else waits for one) and returns it when done, so a rayon-style pool of
+// callers holds at most kMaxStaging x 192 MiB of pinned memory per device, not one set per
+// thread.  The sets are kept for the life of the process.
 struct Staging {
-    bool ok = false;
     char* out[RING] = {};
     hipEvent_t out_ev[RING] = {};
     hipStream_t s_in = nullptr, s_cmp = nullptr, s_out = nullptr;
 };
+constexpr size_t kMaxStaging = 4;
 
-int staging(Staging** out) {
-    thread_local std::map<int, Staging> tl;
-    int dev = 0;
-    HIP_CHECK(hipGetDevice(&dev), "hipGetDevice");
-    Staging& sg = tl[dev];
-    if (!sg.ok) {
-        for (int i = 0; i < RING; i++) {
-            HIP_CHECK(hipHostMalloc((void**)&sg.out[i], SLOT, hipHostMallocDefault), "hipHostMalloc");
-            HIP_CHECK(hipEventCreateWithFlags(&sg.out_ev[i], hipEventDisableTiming), "hipEventCreate");
-        }
-        HIP_CHECK(hipStreamCreateWithFlags(&sg.s_in, hipStreamNonBlocking), "hipStreamCreate");
-        HIP_CHECK(hipStreamCreateWithFlags(&sg.s_cmp, hipStreamNonBlocking), "hipStreamCreate");
-        HIP_CHECK(hipStreamCreateWithFlags(&sg.s_out, hipStreamNonBlocking), "hipStreamCreate");
-        sg.ok = true;
+struct StagingPool {
+    std::mutex mu;
+    std::condition_variable cv;
+    std::map<int, std::vector<Staging*>> free_, all_;
+};
+StagingPool& staging_pool() {
+    static StagingPool* p = new StagingPool();
+    return *p;
+}
+
+int make_staging(Staging* sg) {
+    for (int i = 0; i < RING; i++) {
+        HIP_CHECK(hipHostMalloc((void**)&sg->out[i], SLOT, hipHostMallocDefault), "hipHostMalloc");
+        HIP_CHECK(hipEventCreateWithFlags(&sg->out_ev[i], hipEventDisableTiming), "hipEventCreate");
     }
-    *out = &sg;
+    HIP_CHECK(hipStreamCreateWithFlags(&sg->s_in, hipStreamNonBlocking), "hipStreamCreate");
+    HIP_CHECK(hipStreamCreateWithFlags(&sg->s_cmp, hipStreamNonBlocking), "hipStreamCreate");
+    HIP_CHECK(hipStreamCreateWithFlags(&sg->s_out, hipStreamNonBlocking), "hipStreamCreate");
     return BJ_OK;
 }
+
+// Takes a staging set of the current device for the duration of one call.
+struct StagingLease {
+    Staging* sg = nullptr;
+    int dev = 0;
+    int acquire() {
+        HIP_CHECK(hipGetDevice(&dev), "hipGetDevice");
+        StagingPool& p = staging_pool();
+        std::unique_lock<std::mutex> lk(p.mu);
+        for (;;) {
+            auto& fr = p.free_[dev];
+            if (!fr.empty()) {
+                sg = fr.back();
+                fr.pop_back();
+                return BJ_OK;
+            }
+            if (p.all_[dev].size() < kMaxStaging) break;
+            p.cv.wait(lk);
+        }
+        Staging* s = new Staging();
+        p.all_[dev].push_back(s);  // reserve the slot before dropping the lock
+        lk.unlock();
+        if (int r = make_staging(s)) {
+            // give the slot back; the half-made set's resources are released
+            for (int i = 0; i < RING; i++) {
+                if (s->out[i]) (void)hipHostFree(s->out[i]);
+                if (s->out_ev[i]) (void)hipEventDestroy(s->out_ev[i]);
+            }
+            for (hipStream_t q : {s->s_in, s->s_cmp, s->s_out})
+                if (q) (void)hipStreamDestroy(q);
+            {
+                std::lock_guard<std::mutex> g(p.mu);
+                auto& a = p.all_[dev];
+                a.erase(std::find(a.begin(), a.end(), s));
+            }
+            p.cv.notify_one();
+            delete s;
+            return r;
+        }
+        sg = s;
+        return BJ_OK;
+    }
+    ~StagingLease() {
+        if (!sg) return;
+        StagingPool& p = staging_pool();
+        {
+            std::lock_guard<std::mutex> lk(p.mu);
+            p.free_[dev].push_back(sg);
+        }
+        p.cv.notify_one();
+    }
+};
 
 // Page-locked by the caller (hipHostRegister / hipHostMalloc): DMA it directly.
 bool is_pinned(const void* p) {
@@ -216,12 +273,15 @@ hipError_t d2h(Staging& sg, void* host, const void* dev, size_t bytes, bool pinn
 }  // namespace
 
 extern "C" int bj_lde_commit_h(const uint64_t* trace_h, uint32_t n_cols, uint32_t log_n, uint32_t log_lde,
-                               uint32_t cap_size, uint64_t* lde_h, uint64_t* leaves_h, uint64_t* nodes_h,
-                               uint64_t* cap_h) {
+                               uint32_t log_commit_cosets, uint32_t cap_size, uint64_t* lde_h, uint64_t* leaves_h,
+                               uint64_t* nodes_h, uint64_t* cap_h) {
     if (log_n + log_lde > 32) return err(BJ_EINVAL, "log_n exceeds the 2-adicity (32) of the field");
-    const size_t n = (size_t)1 << log_n, nl = n << log_lde;
+    if (log_commit_cosets > log_lde)
+        return err(BJ_EINVAL, "committed cosets exceed the lde degree (prover.rs:313, lde.rs:298-308)");
+    // nd: LDE length per column (all D cosets); nl: leaves, the first k cosets (subset_for_degree)
+    const size_t n = (size_t)1 << log_n, nd = n << log_lde, nl = n << log_commit_cosets;
     if (!cap_size || (cap_size & (cap_size - 1)) || nl <= cap_size)
-        return err(BJ_EINVAL, "need power-of-two cap_size < n * D");
+        return err(BJ_EINVAL, "need power-of-two cap_size < n * k");
     if (log_lde == 0) return err(BJ_EINVAL, "lde degree must be > 1 (utils.rs:283)");
     if (n_cols && !trace_h) return err(BJ_EINVAL, "null trace");
     // chunk k covers columns [c_first[k], c_first[k + 1]): 8, 8, 16, then 32 at a time (every
@@ -233,30 +293,21 @@ extern "C" int bj_lde_commit_h(const uint64_t* trace_h, uint32_t n_cols, uint32_
         if (c_first.size() == 2) w = 4;  // second chunk 8 as well
     }
     const uint32_t n_chunks = (uint32_t)c_first.size() - 1;
-    Staging* sgp = nullptr;
-    if (int r = staging(&sgp)) return r;
-    Staging& sg = *sgp;
+    StagingLease lease;
+    if (int r = lease.acquire()) return r;
+    Staging& sg = *lease.sg;
     hipStream_t s_in = sg.s_in, s_cmp = sg.s_cmp, s_out = sg.s_out;
-    int dev = 0;
-    HIP_CHECK(hipGetDevice(&dev), "hipGetDevice");
-    {
-        // keep freed pool memory mapped between calls: without this the stream-ordered pool
-        // returns it to the driver at every synchronisation and the next call re-maps the
-        // whole workspace (~20 ms for C2's 5 GB)
-        hipMemPool_t pool;
-        HIP_CHECK(hipDeviceGetDefaultMemPool(&pool, dev), "hipDeviceGetDefaultMemPool");
-        uint64_t keep = UINT64_MAX;
-        HIP_CHECK(hipMemPoolSetAttribute(pool, hipMemPoolAttrReleaseThreshold, &keep), "hipMemPoolSetAttribute");
-    }
+    const int dev = lease.dev;
     const bool pin_lde = lde_h && is_pinned(lde_h);
     const size_t tn = n * n_cols;
-    uint64_t *tr = nullptr, *mono = nullptr, *lde = nullptr, *lv = nullptr, *nd = nullptr, *st = nullptr;
-    HIP_CHECK(hipMallocAsync((void**)&tr, (tn ? tn : 1) * 8, s_cmp), "hipMallocAsync");
-    HIP_CHECK(hipMallocAsync((void**)&mono, (tn ? tn : 1) * 8, s_cmp), "hipMallocAsync");
-    HIP_CHECK(hipMallocAsync((void**)&lde, (tn ? tn << log_lde : 1) * 8, s_cmp), "hipMallocAsync");
-    HIP_CHECK(hipMallocAsync((void**)&lv, nl * 32, s_cmp), "hipMallocAsync");
-    HIP_CHECK(hipMallocAsync((void**)&nd, (nl - cap_size) * 32, s_cmp), "hipMallocAsync");
-    HIP_CHECK(hipMallocAsync((void**)&st, nl * 32, s_cmp), "hipMallocAsync");
+    uint64_t *tr = nullptr, *mono = nullptr, *lde = nullptr, *lv = nullptr, *nodes = nullptr, *st = nullptr;
+    // the library's own stream-ordered pool keeps this workspace mapped between calls
+    HIP_CHECK(bj::pool_alloc((void**)&tr, tn * 8, s_cmp), "pool_alloc");
+    HIP_CHECK(bj::pool_alloc((void**)&mono, tn * 8, s_cmp), "pool_alloc");
+    HIP_CHECK(bj::pool_alloc((void**)&lde, (tn << log_lde) * 8, s_cmp), "pool_alloc");
+    HIP_CHECK(bj::pool_alloc((void**)&lv, nl * 32, s_cmp), "pool_alloc");
+    HIP_CHECK(bj::pool_alloc((void**)&nodes, (nl - cap_size) * 32, s_cmp), "pool_alloc");
+    HIP_CHECK(bj::pool_alloc((void**)&st, nl * 32, s_cmp), "pool_alloc");
     HIP_CHECK(hipStreamSynchronize(s_cmp), "sync");
     struct Frees {
         uint64_t** p[6];
@@ -269,7 +320,7 @@ extern "C" int bj_lde_commit_h(const uint64_t* trace_h, uint32_t n_cols, uint32_
                 if (*q) (void)hipFreeAsync(*q, s);
             (void)hipStreamSynchronize(s);
         }
-    } frees{{&tr, &mono, &lde, &lv, &nd, &st}, s_cmp, s_in, s_out};
+    } frees{{&tr, &mono, &lde, &lv, &nodes, &st}, s_cmp, s_in, s_out};
     std::vector<hipEvent_t> ev_in(n_chunks, nullptr), ev_cmp(n_chunks, nullptr);
     struct Events {
         std::vector<hipEvent_t>* v[2];
@@ -300,7 +351,7 @@ extern "C" int bj_lde_commit_h(const uint64_t* trace_h, uint32_t n_cols, uint32_
             }
             const uint32_t c0 = c_first[k], c = c_first[k + 1] - c0;
             hipError_t e = hipStreamWaitEvent(s_out, ev_cmp[k], 0);
-            if (e == hipSuccess) e = d2h(sg, lde_h + (size_t)c0 * nl, lde + (size_t)c0 * nl, (size_t)c * nl * 8, pin_lde);
+            if (e == hipSuccess) e = d2h(sg, lde_h + (size_t)c0 * nd, lde + (size_t)c0 * nd, (size_t)c * nd * 8, pin_lde);
             if (e != hipSuccess) out_err = e;
         }
     });
@@ -328,10 +379,11 @@ extern "C" int bj_lde_commit_h(const uint64_t* trace_h, uint32_t n_cols, uint32_
                   "memcpy trace");
         HIP_CHECK(hipEventRecord(ev_in[k], s_in), "hipEventRecord");
         HIP_CHECK(hipStreamWaitEvent(s_cmp, ev_in[k], 0), "hipStreamWaitEvent");
-        if (int r = bj_lde_d(tr + (size_t)c0 * n, c, n, log_n, log_lde, mono + (size_t)c0 * n, lde + (size_t)c0 * nl,
+        if (int r = bj_lde_d(tr + (size_t)c0 * n, c, n, log_n, log_lde, mono + (size_t)c0 * n, lde + (size_t)c0 * nd,
                              s_cmp))
             return r;
-        if (int r = bj_merkle_leaves_partial_d(lde + (size_t)c0 * nl, c, nl, nl, k ? st : nullptr, last ? lv : st,
+        // the sponges absorb the chunk's first k cosets (leaf L < k * n of column c at c * nd + L)
+        if (int r = bj_merkle_leaves_partial_d(lde + (size_t)c0 * nd, c, nd, nl, k ? st : nullptr, last ? lv : st,
                                                last ? 1 : 0, s_cmp))
             return r;
         HIP_CHECK(hipEventRecord(ev_cmp[k], s_cmp), "hipEventRecord");
@@ -342,7 +394,7 @@ extern "C" int bj_lde_commit_h(const uint64_t* trace_h, uint32_t n_cols, uint32_
         cv.notify_all();
     }
     if (n_chunks == 0)
-        if (int r = bj_merkle_leaves_d(lde, 0, nl, nl, lv, s_cmp)) return r;
+        if (int r = bj_merkle_leaves_d(lde, 0, nd, nl, lv, s_cmp)) return r;
     hipEvent_t ev_leaves = nullptr, ev_nodes = nullptr;
     HIP_CHECK(hipEventCreateWithFlags(&ev_leaves, hipEventDisableTiming), "hipEventCreate");
     struct Ev {
@@ -353,7 +405,7 @@ extern "C" int bj_lde_commit_h(const uint64_t* trace_h, uint32_t n_cols, uint32_
     } evl{&ev_leaves}, evn{&ev_nodes};
     HIP_CHECK(hipEventCreateWithFlags(&ev_nodes, hipEventDisableTiming), "hipEventCreate");
     HIP_CHECK(hipEventRecord(ev_leaves, s_cmp), "hipEventRecord");
-    if (int r = bj_merkle_nodes_d(lv, nl, cap_size, nd, s_cmp)) return r;
+    if (int r = bj_merkle_nodes_d(lv, nl, cap_size, nodes, s_cmp)) return r;
     HIP_CHECK(hipEventRecord(ev_nodes, s_cmp), "hipEventRecord");
     out_thread.join();
     if (out_err != hipSuccess) return hip_err(out_err, "memcpy lde");
@@ -363,9 +415,9 @@ extern "C" int bj_lde_commit_h(const uint64_t* trace_h, uint32_t n_cols, uint32_
         HIP_CHECK(d2h(sg, leaves_h, lv, nl * 32, is_pinned(leaves_h)), "memcpy leaves");
     }
     HIP_CHECK(hipStreamWaitEvent(s_out, ev_nodes, 0), "hipStreamWaitEvent");
-    if (nodes_h) HIP_CHECK(d2h(sg, nodes_h, nd, (nl - cap_size) * 32, is_pinned(nodes_h)), "memcpy nodes");
+    if (nodes_h) HIP_CHECK(d2h(sg, nodes_h, nodes, (nl - cap_size) * 32, is_pinned(nodes_h)), "memcpy nodes");
     if (cap_h) {
-        HIP_CHECK(hipMemcpyAsync(cap_h, nd + 4 * (nl - 2 * (size_t)cap_size), (size_t)cap_size * 32,
+        HIP_CHECK(hipMemcpyAsync(cap_h, nodes + 4 * (nl - 2 * (size_t)cap_size), (size_t)cap_size * 32,
                                  hipMemcpyDeviceToHost, s_out),
                   "memcpy cap");
     }

@@ -240,20 +240,30 @@ int bj_keccak256_node_h(const uint64_t* left4, const uint64_t* right4, uint64_t*
 
 /* ------------------------------------------------------- whole commitment */
 
-/* Witness commitment, the batched hot path (prover.rs:313-353 with all D cosets
- * committed, fri_lde_factor == lde degree): LDE of every column, Poseidon2 leaves over
- * the n*D rows, node levels to the cap.  All pointers device; cap additionally copied
- * to cap_h (host, cap_size x 4) if non-NULL (this synchronises the stream). */
+/* Witness commitment, the batched hot path (prover.rs:313-353): the LDE of every column at
+ * D = 2^log_lde (used_lde_degree = max(fri_lde_factor, quotient_degree), prover.rs:313), then
+ * MerkleTreeWithCap::construct over the first k = 2^log_commit_cosets cosets only
+ * (source = subset_for_degree(fri_lde_factor), prover.rs:325-347, polynomial/lde.rs:298-308):
+ * leaf L = coset * n + row < k * n, node levels to the cap.  log_commit_cosets <= log_lde; the
+ * reference's own proof.json is D = 8 (quotient degree), k = 2 (fri_lde_factor).
+ *   scratch  n_cols x n (monomials, as bj_lde_d)
+ *   lde      n_cols x D x n, all D cosets (as bj_lde_d)
+ *   leaves   k*n x 4;  nodes (k*n - cap_size) x 4, the cap being the last cap_size digests
+ * All pointers device; cap additionally copied to cap_h (host, cap_size x 4) if non-NULL
+ * (this synchronises the stream).  Requires power-of-two cap_size < k * n. */
 int bj_lde_commit_d(const uint64_t* trace, uint32_t n_cols, size_t trace_stride, uint32_t log_n,
-                    uint32_t log_lde, uint32_t cap_size, uint64_t* scratch, uint64_t* lde,
-                    uint64_t* leaves, uint64_t* nodes, uint64_t* cap_h, void* stream);
+                    uint32_t log_lde, uint32_t log_commit_cosets, uint32_t cap_size, uint64_t* scratch,
+                    uint64_t* lde, uint64_t* leaves, uint64_t* nodes, uint64_t* cap_h, void* stream);
 
-/* Host-buffer variant (drop-in for a Rust prover that owns host Vecs): copies the trace
- * in, runs bj_lde_commit_d, copies every output back.  Any output pointer may be NULL
- * to skip its copy.  PCIe-inclusive; never the headline number. */
+/* Host-buffer variant (drop-in for a Rust prover that owns host Vecs): the trace goes in,
+ * bj_lde_commit_d's pipeline runs column chunk by column chunk, every output comes back (lde_h
+ * n_cols x D x n, leaves_h k*n x 4, nodes_h, cap_h).  Any output pointer may be NULL to skip its
+ * copy.  Device workspace comes from the library's own stream-ordered pool (the process's default
+ * pool is not touched); pinned staging (3 x 64 MiB + 3 streams per set) comes from a per-device
+ * pool of at most 4 sets shared by all calling threads.  PCIe-inclusive; never the headline. */
 int bj_lde_commit_h(const uint64_t* trace_h, uint32_t n_cols, uint32_t log_n, uint32_t log_lde,
-                    uint32_t cap_size, uint64_t* lde_h, uint64_t* leaves_h, uint64_t* nodes_h,
-                    uint64_t* cap_h);
+                    uint32_t log_commit_cosets, uint32_t cap_size, uint64_t* lde_h, uint64_t* leaves_h,
+                    uint64_t* nodes_h, uint64_t* cap_h);
 
 /* ------------------------------------- collective sharded commit (8(b), 8(e)) */
 /* The whole G-rank witness commitment as one collective call per rank: one process (or
@@ -272,16 +282,30 @@ int bj_lde_commit_h(const uint64_t* trace_h, uint32_t n_cols, uint32_t log_n, ui
  *   bj_comm_wrap_rccl       an ncclComm_t the caller already owns (not destroyed by us);
  *   bj_comm_local_*         in-process ranks that share one device (threads; device-to-device
  *                           copies through a host barrier): a rehearsal transport that runs the
- *                           same pipeline multi-rank on one GPU.  Not for performance.
+ *                           same pipeline multi-rank on one GPU.  Not for performance.  If a rank
+ *                           fails mid-collective the group is aborted: its peers return an error
+ *                           instead of waiting, and the group must be destroyed;
+ *   bj_comm_init_callback   the caller's own exchange (gloo, MPI, a test double), called for
+ *                           every data exchange from the thread that called the collective.
+ *                           kind BJ_XCHG_ALL_GATHER: recv (world x bytes) <- concat over ranks of
+ *                           send (bytes); BJ_XCHG_ALL_TO_ALL: recv block p (bytes) <- block `rank`
+ *                           of rank p's send (world x bytes).  host_staged != 0: send / recv are
+ *                           host buffers (the library synchronises, copies out, calls, copies
+ *                           back; stream is NULL).  host_staged == 0: device pointers, and the
+ *                           exchange must be ordered on `stream`.  Returns 0 on success.
  * RCCL is resolved at run time (dlopen of librccl.so.1, reusing an already loaded copy), so the
  * library loads without it.  All ranks must call collectives in the same order. */
 typedef struct bj_comm bj_comm;
+#define BJ_XCHG_ALL_GATHER 0
+#define BJ_XCHG_ALL_TO_ALL 1
+typedef int (*bj_exchange_fn)(void* user, int kind, const void* send, void* recv, size_t bytes, void* stream);
 int bj_comm_rccl_unique_id(uint8_t* id_out128);
 int bj_comm_init_rccl(const uint8_t* id128, int world, int rank, bj_comm** out);
 int bj_comm_wrap_rccl(void* nccl_comm, int world, int rank, bj_comm** out);
 int bj_comm_local_group_create(int world, void** group_out);
 int bj_comm_local_group_destroy(void* group);
 int bj_comm_init_local(void* group, int rank, bj_comm** out);
+int bj_comm_init_callback(int world, int rank, bj_exchange_fn exchange, void* user, int host_staged, bj_comm** out);
 int bj_comm_destroy(bj_comm* comm);
 
 #define BJ_HASHER_POSEIDON2 0
@@ -297,30 +321,41 @@ int bj_comm_destroy(bj_comm* comm);
 int bj_sharded_columns(uint32_t n_cols, uint32_t log_shards, uint32_t shard, int hasher, uint32_t* cols_out);
 
 /* Rank P's part of the G-way commit (G = the communicator's world, a power of two; P its rank).
+ * The LDE is at D = 2^log_lde, the tree over the first k = 2^log_commit_cosets cosets
+ * (bj_lde_commit_d; prover.rs:313-347).  The committed domain of m_k = k * n leaves is cut into
+ * G ranges of m = k * n / G; rank P owns leaf range [P * m, (P + 1) * m) and, so that the LDE
+ * work stays balanced, the same range of every other block of k cosets: block j (cosets
+ * [j*k, (j+1)*k), j < B = D / k) of the D-coset LDE is itself a k-coset LDE with an extra shift,
+ * and rank P holds its part [P * m, (P + 1) * m).
  * trace_shard: n_cols / G columns of n = 2^log_n in bj_sharded_columns order at
  *              trace_shard + j * trace_stride (device, read only).
- * Outputs (device, this rank's shard of the reference's tree; m = n * 2^log_lde / G leaves,
- * flat leaf range [P * m, (P + 1) * m) of coset * n + row):
- *   lde    n_cols x m, global column c at lde + c * m;
+ * Outputs (device):
+ *   lde    B x n_cols x m: block j, global column c at lde + (j * n_cols + c) * m; block 0 is the
+ *          committed one, equal to lde_full[c][P*m .. (P+1)*m) of bj_lde_commit_d's flat
+ *          coset * n + row index; block j to lde_full[c][j*k*n + P*m ..];
  *   leaves m x 4;
  *   nodes  (m - cap_local) x 4, the subtree levels, cap_local = max(1, cap_size / G);
  *   cap    cap_size x 4, the full gathered cap (identical on every rank).
- * Requires n_cols % G == 0, log_lde >= 1, power-of-two cap_size < n * D, m > cap_local.
- * Asynchronous on `stream`; workspace comes from the stream-ordered pool. */
+ * Exchange: G <= D all-gather of the coefficients (8 n n_cols bytes in total); G > D the sender
+ * folds its columns for every (block, rank) and all-to-alls deliver them (8 n D / G n_cols bytes
+ * received per rank).  Requires n_cols % G == 0, log_lde >= 1, log_commit_cosets <= log_lde,
+ * G <= k * n, G / k <= 64, power-of-two cap_size < k * n, m > cap_local.  Asynchronous on
+ * `stream`; workspace comes from the library's stream-ordered pool. */
 int bj_sharded_commit_d(bj_comm* comm, const uint64_t* trace_shard, size_t trace_stride, uint32_t n_cols,
-                        uint32_t log_n, uint32_t log_lde, uint32_t cap_size, int hasher, uint64_t* lde,
-                        uint64_t* leaves, uint64_t* nodes, uint64_t* cap, void* stream);
+                        uint32_t log_n, uint32_t log_lde, uint32_t log_commit_cosets, uint32_t cap_size,
+                        int hasher, uint64_t* lde, uint64_t* leaves, uint64_t* nodes, uint64_t* cap, void* stream);
 
-/* OracleQuery::construct (proof.rs:65-97) on a bj_sharded_commit_d commit: tree index idx (flat
- * leaf index coset * n + row) of the global tree.  The owning rank reads the row of every
- * column and its subtree path; when cap_size < G the top levels over the gathered subtree roots
- * finish the path on every rank.  Collective: every rank passes its own commit outputs and the
- * same idx, and every rank receives, in host memory, leaf_elements (n_cols), leaf_hash (4) and
- * proof (depth x 4, depth = log2(n * D / cap_size), MerkleTreeWithCap::get_proof order,
- * merkle_tree.rs:462-480).  Synchronous. */
+/* OracleQuery::construct (proof.rs:65-97) on a bj_sharded_commit_d commit: tree index idx < k * n
+ * (flat leaf index coset * n + row of the committed cosets) of the global tree.  The owning rank
+ * reads the row of every column and its subtree path; when cap_size < G the top levels over the
+ * gathered subtree roots finish the path on every rank.  Collective: every rank passes its own
+ * commit outputs and the same idx, and every rank receives, in host memory, leaf_elements
+ * (n_cols), leaf_hash (4) and proof (depth x 4, depth = log2(k * n / cap_size),
+ * MerkleTreeWithCap::get_proof order, merkle_tree.rs:462-480).  Synchronous. */
 int bj_sharded_query_h(bj_comm* comm, const uint64_t* lde, const uint64_t* leaves, const uint64_t* nodes,
-                       uint32_t n_cols, uint32_t log_n, uint32_t log_lde, uint32_t cap_size, int hasher, uint64_t idx,
-                       uint64_t* leaf_elements_h, uint64_t* leaf_hash_h, uint64_t* proof_h, void* stream);
+                       uint32_t n_cols, uint32_t log_n, uint32_t log_lde, uint32_t log_commit_cosets,
+                       uint32_t cap_size, int hasher, uint64_t idx, uint64_t* leaf_elements_h,
+                       uint64_t* leaf_hash_h, uint64_t* proof_h, void* stream);
 
 /* ------------------------------------------------------------------- FRI */
 
@@ -330,8 +365,9 @@ int bj_sharded_query_h(bj_comm* comm, const uint64_t* lde, const uint64_t* leave
  *   dst_i = f(x) + f(-x) + alpha * (f(x) - f(-x)) * roots[i] * coset_inverse,  i < n_src / 2,
  * f(x) = (c0[2i], c1[2i]), f(-x) = (c0[2i+1], c1[2i+1]), alpha = (ch0, ch1), u^2 = 7.
  * roots: the INVERSED bit-reversed twiddles of the full FRI domain (bj_precompute_twiddles_d
- * with inverse = 1), indexed by the flat pair index.  Device pointers (c0, c1 16-byte aligned:
- * each (f(x), f(-x)) pair is one load); outputs canonical. */
+ * with inverse = 1), indexed by the flat pair index.  Device pointers; outputs canonical.
+ * c0 / c1 at 16-byte-aligned addresses load each (f(x), f(-x)) pair as one 16-byte load; any
+ * other 8-byte-aligned address runs the same fold with 8-byte loads. */
 int bj_fri_fold_d(const uint64_t* c0, const uint64_t* c1, size_t n_src, const uint64_t* roots,
                   uint64_t coset_inverse, uint64_t ch0, uint64_t ch1, uint64_t* dst_c0, uint64_t* dst_c1,
                   void* stream);

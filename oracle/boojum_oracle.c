@@ -622,10 +622,17 @@ static void node_job(void* c, size_t b, size_t e) {
  * leaves: n_leaves x 4.  nodes: all node levels from the leaves up to and including
  * the cap level, concatenated (n_leaves/2 + n_leaves/4 + ... + cap_size) x 4
  * (node_hashes_enumerated_from_leafs, :388-449).  Returns the number of node levels. */
-int bjo_merkle_construct_with(const u64* lde, size_t col_stride, uint32_t n_cols, size_t n_leaves,
-                              uint32_t cap_size, u64* leaves, u64* nodes, int threads, int hasher) {
+/* The leaf hashes alone (the reference's leaf loop, :112-157) ... */
+void bjo_merkle_leaves_with(const u64* lde, size_t col_stride, uint32_t n_cols, size_t n_leaves, u64* leaves,
+                            int threads, int hasher) {
     mk_ctx_t x = {lde, col_stride, n_cols, leaves, NULL, NULL, hasher};
     worker_scope(threads, n_leaves, leaf_job, &x);
+}
+
+/* ... and the node levels over them (continue_from_leaf_hashes, :388-449). */
+int bjo_merkle_nodes_with(const u64* leaves, size_t n_leaves, uint32_t cap_size, u64* nodes, int threads,
+                          int hasher) {
+    mk_ctx_t x = {NULL, 0, 0, NULL, NULL, NULL, hasher};
     int levels = 0;
     const u64* prev = leaves;
     u64* out = nodes;
@@ -635,6 +642,12 @@ int bjo_merkle_construct_with(const u64* lde, size_t col_stride, uint32_t n_cols
         prev = out; out += 4 * (len / 2); levels++;
     }
     return levels;
+}
+
+int bjo_merkle_construct_with(const u64* lde, size_t col_stride, uint32_t n_cols, size_t n_leaves,
+                              uint32_t cap_size, u64* leaves, u64* nodes, int threads, int hasher) {
+    bjo_merkle_leaves_with(lde, col_stride, n_cols, n_leaves, leaves, threads, hasher);
+    return bjo_merkle_nodes_with(leaves, n_leaves, cap_size, nodes, threads, hasher);
 }
 
 int bjo_merkle_construct(const u64* lde, size_t col_stride, uint32_t n_cols, size_t n_leaves,
@@ -682,14 +695,18 @@ int bjo_verify_proof_over_cap(const u64* path, int levels, const u64* cap, const
 
 /* ---------------------------------------------------- whole commit (a21) */
 
-/* Witness commit as prover.rs:313-353 with fri_lde_factor == lde degree (all
- * cosets committed): LDE of every column, Merkle tree over the n*D rows, cap.
- * trace is overwritten with the monomials.  cap_out: cap_size x 4. */
-int bjo_lde_commit(u64* trace, uint32_t n_cols, uint32_t log_n, uint32_t log_d, uint32_t cap_size,
-                   u64* lde, u64* leaves, u64* nodes, u64* cap_out, int threads) {
-    size_t n = (size_t)1 << log_n, nl = n << log_d;
+/* Witness commit as prover.rs:313-353: the LDE of every column at D = 2^log_d
+ * (used_lde_degree = max(fri_lde_factor, quotient_degree), prover.rs:313, via
+ * WitnessStorage::from_base_trace_ext, prover.rs:316-323), then the Merkle tree over
+ * subset_for_degree(fri_lde_factor) of every column (prover.rs:325-347): the first
+ * k = 2^log_k cosets (polynomial/lde.rs:298-308), i.e. leaf L < k * n of column c is
+ * lde[c * D * n + L].  trace is overwritten with the monomials.  lde: n_cols x D x n;
+ * leaves: k*n x 4; nodes: (k*n - cap) x 4; cap_out: cap_size x 4. */
+int bjo_lde_commit_subset(u64* trace, uint32_t n_cols, uint32_t log_n, uint32_t log_d, uint32_t log_k,
+                          uint32_t cap_size, u64* lde, u64* leaves, u64* nodes, u64* cap_out, int threads) {
+    size_t n = (size_t)1 << log_n, nd = n << log_d, nl = n << log_k;
     bjo_lde(trace, n_cols, log_n, log_d, lde, threads);
-    int levels = bjo_merkle_construct(lde, nl, n_cols, nl, cap_size, leaves, nodes, threads);
+    int levels = bjo_merkle_construct(lde, nd, n_cols, nl, cap_size, leaves, nodes, threads);
     const u64* top = leaves;
     if (levels > 0) {
         size_t off = 0, len = nl;
@@ -698,6 +715,12 @@ int bjo_lde_commit(u64* trace, uint32_t n_cols, uint32_t log_n, uint32_t log_d, 
     }
     memcpy(cap_out, top, sizeof(u64) * 4 * cap_size);
     return levels;
+}
+
+/* All D cosets committed (fri_lde_factor == lde degree). */
+int bjo_lde_commit(u64* trace, uint32_t n_cols, uint32_t log_n, uint32_t log_d, uint32_t cap_size,
+                   u64* lde, u64* leaves, u64* nodes, u64* cap_out, int threads) {
+    return bjo_lde_commit_subset(trace, n_cols, log_n, log_d, log_d, cap_size, lde, leaves, nodes, cap_out, threads);
 }
 
 /* Brute-force search for the leaf index of a proof.json query (fixture tool):

@@ -51,6 +51,8 @@ def lib():
         L.bjo_verify_proof_over_cap.argtypes = [_u64p, i, _u64p, _u64p, sz]
         L.bjo_lde_commit.restype = i
         L.bjo_lde_commit.argtypes = [_u64p, u32, u32, u32, u32, _u64p, _u64p, _u64p, _u64p, i]
+        L.bjo_lde_commit_subset.restype = i
+        L.bjo_lde_commit_subset.argtypes = [_u64p, u32, u32, u32, u32, u32, _u64p, _u64p, _u64p, _u64p, i]
         L.bjo_blake2s.argtypes = [ctypes.c_char_p, sz, ctypes.c_char_p]
         L.bjo_blake2s_leaf.argtypes = [_u64p, sz, _u64p]
         L.bjo_blake2s_node.argtypes = [_u64p, _u64p, _u64p]
@@ -58,6 +60,9 @@ def lib():
         L.bjo_keccak256.argtypes = [ctypes.c_char_p, sz, ctypes.c_char_p, i]
         L.bjo_keccak_leaf.argtypes = [_u64p, sz, _u64p]
         L.bjo_keccak_node.argtypes = [_u64p, _u64p, _u64p]
+        L.bjo_merkle_leaves_with.argtypes = [_u64p, sz, u32, sz, _u64p, i, i]
+        L.bjo_merkle_nodes_with.restype = i
+        L.bjo_merkle_nodes_with.argtypes = [_u64p, sz, u32, _u64p, i, i]
         L.bjo_merkle_construct_with.restype = i
         L.bjo_merkle_construct_with.argtypes = [_u64p, sz, u32, sz, u32, _u64p, _u64p, i, i]
         L.bjo_verify_proof_over_cap_with.restype = i
@@ -269,6 +274,26 @@ def merkle_construct(lde_flat, cap_size, threads=1, hasher="poseidon2"):
     return leaves, nodes[:n_nodes], levels, cap
 
 
+def merkle_construct_timed(lde_flat, cap_size, threads=1, hasher="poseidon2"):
+    """merkle_construct with the reference's own phase split (merkle_tree.rs:162-167 leaf timing,
+    :438-442 node timing): returns (leaves, nodes, levels, cap, {"leaves": s, "nodes": s})."""
+    import time
+    src = _u64(lde_flat)
+    c, nl = src.shape
+    levels = num_node_levels(nl, cap_size)
+    leaves = np.zeros((nl, 4), dtype=np.uint64)
+    n_nodes = nl - cap_size if levels > 0 else 0
+    nodes = np.zeros((max(n_nodes, 1), 4), dtype=np.uint64)
+    t0 = time.perf_counter()
+    lib().bjo_merkle_leaves_with(_p(src), nl, c, nl, _p(leaves), threads, HASHERS[hasher])
+    t1 = time.perf_counter()
+    got = lib().bjo_merkle_nodes_with(_p(leaves), nl, cap_size, _p(nodes), threads, HASHERS[hasher])
+    t2 = time.perf_counter()
+    assert got == levels
+    cap = nodes[n_nodes - cap_size: n_nodes].copy() if levels > 0 else leaves.copy()
+    return leaves, nodes[:n_nodes], levels, cap, {"leaves": t1 - t0, "nodes": t2 - t1}
+
+
 def merkle_construct_by_chunking(sources_flat, elements_per_leaf, cap_size, threads=1, hasher="poseidon2"):
     """MerkleTreeWithCap::construct_by_chunking / construct_by_chunking_from_flat_sources
     (merkle_tree.rs:176-386): leaf L hashes, for each source c in order, the E consecutive
@@ -298,19 +323,22 @@ def verify_proof_over_cap(path, cap, leaf, idx, hasher="poseidon2"):
                                                      HASHERS[hasher]))
 
 
-def lde_commit(trace, log_d, cap_size, threads=1):
-    """Full witness commit (oracle).  Returns dict with monomials, lde (C, D, n),
-    leaves, nodes, cap."""
-    tr = _u64(trace).copy()
+def lde_commit(trace, log_d, cap_size, threads=1, log_k=None, in_place=False):
+    """Full witness commit (oracle, prover.rs:313-347): LDE at 2^log_d, tree over the first
+    2^log_k cosets (subset_for_degree; default all).  Returns dict with monomials, lde (C, D, n),
+    leaves (k n, 4), nodes, cap.  in_place: the trace array itself becomes the monomials."""
+    tr = _u64(trace) if in_place else _u64(trace).copy()
     c, n = tr.shape
     log_n = n.bit_length() - 1
-    nl = n << log_d
+    log_k = log_d if log_k is None else log_k
+    nl = n << log_k
     lde_out = np.zeros((c, 1 << log_d, n), dtype=np.uint64)
     leaves = np.zeros((nl, 4), dtype=np.uint64)
     n_nodes = nl - cap_size
     nodes = np.zeros((max(n_nodes, 1), 4), dtype=np.uint64)
     cap = np.zeros((cap_size, 4), dtype=np.uint64)
-    lib().bjo_lde_commit(_p(tr), c, log_n, log_d, cap_size, _p(lde_out), _p(leaves), _p(nodes), _p(cap), threads)
+    lib().bjo_lde_commit_subset(_p(tr), c, log_n, log_d, log_k, cap_size, _p(lde_out), _p(leaves), _p(nodes),
+                                _p(cap), threads)
     return {"monomials": tr, "lde": lde_out, "leaves": leaves, "nodes": nodes[:n_nodes], "cap": cap}
 
 

@@ -1,9 +1,9 @@
 #!/bin/bash
 # rocprofv3 evidence for the C3 bench: the default bench line (with the CPU baseline), a
 # kernel-trace stats run, then one PMC pass per counter group.
-# usage: bash scripts/profile_r1.sh TAG
+# usage: bash scripts/profile.sh TAG
 set -u
-TAG=${1:-r1}
+TAG=${1:-r2}
 cd "$GRAFT_REPO_ROOT"
 export TMPDIR=/tmp
 OUT=gpurun_out/prof_$TAG

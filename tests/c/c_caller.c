@@ -12,11 +12,15 @@
  *      (an earlier null-stream version of the seam returned a stale column about every other run);
  *   2. TreeHasher leaf/node (cs/oracle/mod.rs:141-168);
  *   3. the whole witness commit through the host-buffer entry point bj_lde_commit_h
- *      (prover.rs:313-353): LDE, leaves, nodes and cap bit-exact;
- *   4. the error contract: a violated precondition (fft/mod.rs:399-402 asserts a power-of-two
+ *      (prover.rs:313-353): LDE at D, tree over the first k cosets (subset_for_degree,
+ *      prover.rs:325-347); LDE, leaves, nodes and cap bit-exact;
+ *   4. the collective sharded commit (bj_sharded_commit_d) at G = 2, 4, 8 ranks as threads on
+ *      one device, with the same D / k split;
+ *   5. the error contract: a violated precondition (fft/mod.rs:399-402 asserts a power-of-two
  *      length) returns BJ_EINVAL with a message, and the library keeps working.
  *
- * usage: c_caller LOG_N N_COLS LOG_LDE CAP THREADS      prints "c_caller ok ..." on success
+ * usage: c_caller LOG_N N_COLS LOG_LDE CAP THREADS [LOG_K]   prints "c_caller ok ..." on success
+ *        (LOG_K = log2 of the committed cosets, default LOG_LDE)
  */
 #include <pthread.h>
 #include <stdint.h>
@@ -39,8 +43,8 @@ void bjo_fft_natural_to_bitreversed(u64* a, size_t n, u64 coset, const u64* tw);
 void bjo_ifft_natural_to_natural(u64* a, size_t n, u64 coset, const u64* inv_tw);
 void bjo_hash_into_leaf(const u64* elems, size_t count, u64* out4);
 void bjo_hash_into_node(const u64* l, const u64* r, u64* out4);
-int bjo_lde_commit(u64* trace, uint32_t n_cols, uint32_t log_n, uint32_t log_d, uint32_t cap_size, u64* lde,
-                   u64* leaves, u64* nodes, u64* cap_out, int threads);
+int bjo_lde_commit_subset(u64* trace, uint32_t n_cols, uint32_t log_n, uint32_t log_d, uint32_t log_k,
+                          uint32_t cap_size, u64* lde, u64* leaves, u64* nodes, u64* cap_out, int threads);
 
 static int failures = 0;
 #define CHECK(cond, ...)                      \
@@ -165,20 +169,20 @@ static void check_tree_hasher(void) {
 
 /* ------------------------------------------------------ 3. whole witness commit */
 
-static void check_commit(uint32_t log_n, uint32_t n_cols, uint32_t log_lde, uint32_t cap, int threads,
+static void check_commit(uint32_t log_n, uint32_t n_cols, uint32_t log_lde, uint32_t log_k, uint32_t cap, int threads,
                          u64* cap_out) {
-    size_t n = (size_t)1 << log_n, nl = n << log_lde, n_nodes = nl - cap;
+    size_t n = (size_t)1 << log_n, nd = n << log_lde, nl = n << log_k, n_nodes = nl - cap;
     u64* trace = xmalloc(8 * n * n_cols);
     for (uint32_t c = 0; c < n_cols; c++)
         for (size_t r = 0; r < n; r++) trace[(size_t)c * n + r] = canon(splitmix64(42 + (u64)c * n + r));
-    u64* lde = xmalloc(8 * nl * n_cols), *leaves = xmalloc(32 * nl), *nodes = xmalloc(32 * n_nodes);
-    int rc = bj_lde_commit_h(trace, n_cols, log_n, log_lde, cap, lde, leaves, nodes, cap_out);
+    u64* lde = xmalloc(8 * nd * n_cols), *leaves = xmalloc(32 * nl), *nodes = xmalloc(32 * n_nodes);
+    int rc = bj_lde_commit_h(trace, n_cols, log_n, log_lde, log_k, cap, lde, leaves, nodes, cap_out);
     CHECK(rc == BJ_OK, "bj_lde_commit_h: rc %d (%s)", rc, bj_last_error());
-    u64* r_lde = xmalloc(8 * nl * n_cols), *r_leaves = xmalloc(32 * nl), *r_nodes = xmalloc(32 * n_nodes);
+    u64* r_lde = xmalloc(8 * nd * n_cols), *r_leaves = xmalloc(32 * nl), *r_nodes = xmalloc(32 * n_nodes);
     u64 r_cap[4 * 4096];
-    bjo_lde_commit(trace, n_cols, log_n, log_lde, cap, r_lde, r_leaves, r_nodes, r_cap, threads);
+    bjo_lde_commit_subset(trace, n_cols, log_n, log_lde, log_k, cap, r_lde, r_leaves, r_nodes, r_cap, threads);
     size_t w = 0;
-    CHECK(eq_canon(lde, r_lde, nl * n_cols, &w), "LDE differs at %zu", w);
+    CHECK(eq_canon(lde, r_lde, nd * n_cols, &w), "LDE differs at %zu", w);
     CHECK(eq_canon(leaves, r_leaves, 4 * nl, &w), "leaves differ at %zu", w);
     CHECK(eq_canon(nodes, r_nodes, 4 * n_nodes, &w), "nodes differ at %zu", w);
     CHECK(eq_canon(cap_out, r_cap, 4 * cap, &w), "cap differs at %zu", w);
@@ -190,7 +194,7 @@ static void check_commit(uint32_t log_n, uint32_t n_cols, uint32_t log_lde, uint
 typedef struct {
     void* group;
     int rank, world;
-    uint32_t n_cols, log_n, log_lde, cap;
+    uint32_t n_cols, log_n, log_lde, log_k, cap;
     const u64* trace; /* all columns, host */
     u64* leaves;      /* all leaves, host: rank P writes its range */
     u64* cap_out;     /* this rank's gathered cap */
@@ -211,7 +215,9 @@ typedef struct {
  * transport here; with RCCL each would own a GPU (bj_comm_init_rccl). */
 static void* rank_worker(void* p) {
     rank_job_t* j = (rank_job_t*)p;
-    const size_t n = (size_t)1 << j->log_n, nl = n << j->log_lde, m = nl / j->world;
+    /* m leaves per rank over the first k cosets; its LDE is D / k blocks of m per column */
+    const size_t n = (size_t)1 << j->log_n, nl = n << j->log_k, m = nl / j->world;
+    const size_t blocks = (size_t)1 << (j->log_lde - j->log_k);
     const uint32_t cpr = j->n_cols / j->world, cap_local = j->cap / j->world ? j->cap / j->world : 1;
     uint32_t log_g = 0;
     while ((1 << log_g) < j->world) log_g++;
@@ -223,7 +229,7 @@ static void* rank_worker(void* p) {
     HIPC(hipStreamCreate(&st));
     u64 *tr, *lde, *leaves, *nodes, *cap;
     HIPC(hipMalloc((void**)&tr, 8 * n * cpr));
-    HIPC(hipMalloc((void**)&lde, 8 * m * j->n_cols));
+    HIPC(hipMalloc((void**)&lde, 8 * m * j->n_cols * blocks));
     HIPC(hipMalloc((void**)&leaves, 32 * m));
     HIPC(hipMalloc((void**)&nodes, 32 * (m - cap_local)));
     HIPC(hipMalloc((void**)&cap, 32 * j->cap));
@@ -231,8 +237,8 @@ static void* rank_worker(void* p) {
     bj_comm* comm = NULL;
     j->rc = bj_comm_init_local(j->group, j->rank, &comm);
     if (j->rc) return NULL;
-    j->rc = bj_sharded_commit_d(comm, tr, n, j->n_cols, j->log_n, j->log_lde, j->cap, BJ_HASHER_POSEIDON2, lde,
-                                leaves, nodes, cap, st);
+    j->rc = bj_sharded_commit_d(comm, tr, n, j->n_cols, j->log_n, j->log_lde, j->log_k, j->cap, BJ_HASHER_POSEIDON2,
+                                lde, leaves, nodes, cap, st);
     if (j->rc == 0) {
         HIPC(hipStreamSynchronize(st));
         HIPC(hipMemcpy(j->leaves + 4 * m * j->rank, leaves, 32 * m, hipMemcpyDeviceToHost));
@@ -245,8 +251,8 @@ static void* rank_worker(void* p) {
     return NULL;
 }
 
-static void check_sharded(uint32_t log_n, uint32_t n_cols, uint32_t log_lde, uint32_t cap, int world) {
-    size_t n = (size_t)1 << log_n, nl = n << log_lde, n_nodes = nl - cap;
+static void check_sharded(uint32_t log_n, uint32_t n_cols, uint32_t log_lde, uint32_t log_k, uint32_t cap, int world) {
+    size_t n = (size_t)1 << log_n, nd = n << log_lde, nl = n << log_k, n_nodes = nl - cap;
     u64* trace = xmalloc(8 * n * n_cols);
     for (uint32_t c = 0; c < n_cols; c++)
         for (size_t r = 0; r < n; r++) trace[(size_t)c * n + r] = canon(splitmix64(42 + (u64)c * n + r));
@@ -258,7 +264,8 @@ static void check_sharded(uint32_t log_n, uint32_t n_cols, uint32_t log_lde, uin
     pthread_t th[64];
     rank_job_t jobs[64];
     for (int P = 0; P < world; P++) {
-        jobs[P] = (rank_job_t){group, P, world, n_cols, log_n, log_lde, cap, trace, leaves, caps + 4 * (size_t)cap * P, 0};
+        jobs[P] = (rank_job_t){group, P, world, n_cols, log_n, log_lde, log_k, cap, trace, leaves,
+                               caps + 4 * (size_t)cap * P, 0};
         pthread_create(&th[P], NULL, rank_worker, &jobs[P]);
     }
     for (int P = 0; P < world; P++) {
@@ -266,9 +273,9 @@ static void check_sharded(uint32_t log_n, uint32_t n_cols, uint32_t log_lde, uin
         CHECK(jobs[P].rc == 0, "rank %d of %d: rc %d", P, world, jobs[P].rc);
     }
     bj_comm_local_group_destroy(group);
-    u64* r_lde = xmalloc(8 * nl * n_cols), *r_leaves = xmalloc(32 * nl), *r_nodes = xmalloc(32 * n_nodes);
+    u64* r_lde = xmalloc(8 * nd * n_cols), *r_leaves = xmalloc(32 * nl), *r_nodes = xmalloc(32 * n_nodes);
     u64 r_cap[4 * 4096];
-    bjo_lde_commit(trace, n_cols, log_n, log_lde, cap, r_lde, r_leaves, r_nodes, r_cap, 4);
+    bjo_lde_commit_subset(trace, n_cols, log_n, log_lde, log_k, cap, r_lde, r_leaves, r_nodes, r_cap, 4);
     size_t w = 0;
     CHECK(eq_canon(leaves, r_leaves, 4 * nl, &w), "sharded x%d leaves differ at %zu", world, w);
     for (int P = 0; P < world; P++)
@@ -287,31 +294,33 @@ static void check_errors(void) {
 }
 
 int main(int argc, char** argv) {
-    if (argc != 6) {
-        fprintf(stderr, "usage: %s LOG_N N_COLS LOG_LDE CAP THREADS\n", argv[0]);
+    if (argc != 6 && argc != 7) {
+        fprintf(stderr, "usage: %s LOG_N N_COLS LOG_LDE CAP THREADS [LOG_K]\n", argv[0]);
         return 2;
     }
     uint32_t log_n = atoi(argv[1]), n_cols = atoi(argv[2]), log_lde = atoi(argv[3]), cap = atoi(argv[4]);
     int threads = atoi(argv[5]);
-    if (cap == 0 || cap > 4096 || (cap & (cap - 1)) || threads < 1) {
-        fprintf(stderr, "cap must be a power of two <= 4096, threads >= 1\n");
+    uint32_t log_k = argc == 7 ? (uint32_t)atoi(argv[6]) : log_lde;
+    if (cap == 0 || cap > 4096 || (cap & (cap - 1)) || threads < 1 || log_k > log_lde) {
+        fprintf(stderr, "cap must be a power of two <= 4096, threads >= 1, LOG_K <= LOG_LDE\n");
         return 2;
     }
     fprintf(stderr, "abi %u.%u\n", bj_abi_version() >> 16, bj_abi_version() & 0xffff);
     for (int round = 0; round < 3; round++) check_fft_seam(log_n, n_cols, threads);
     check_tree_hasher();
     u64 cap_out[4 * 4096];
-    check_commit(log_n, n_cols, log_lde, cap, threads, cap_out);
+    check_commit(log_n, n_cols, log_lde, log_k, cap, threads, cap_out);
     for (int world = 2; world <= 8; world *= 2)
-        if (n_cols % world == 0 && ((size_t)1 << (log_n + log_lde)) / world > (cap / world ? cap / world : 1))
-            check_sharded(log_n, n_cols, log_lde, cap, world);
+        if (n_cols % world == 0 && ((size_t)1 << (log_n + log_k)) / world > (cap / world ? cap / world : 1))
+            check_sharded(log_n, n_cols, log_lde, log_k, cap, world);
     check_errors();
     if (failures) {
         fprintf(stderr, "%d check(s) failed\n", failures);
         return 1;
     }
-    printf("c_caller ok: 2^%u x %u, LDE x%u, cap %u, %d seam threads; cap[0] = %016llx %016llx %016llx %016llx\n",
-           log_n, n_cols, 1u << log_lde, cap, threads, (unsigned long long)canon(cap_out[0]),
+    printf("c_caller ok: 2^%u x %u, LDE x%u, %u cosets committed, cap %u, %d seam threads; "
+           "cap[0] = %016llx %016llx %016llx %016llx\n",
+           log_n, n_cols, 1u << log_lde, 1u << log_k, cap, threads, (unsigned long long)canon(cap_out[0]),
            (unsigned long long)canon(cap_out[1]), (unsigned long long)canon(cap_out[2]),
            (unsigned long long)canon(cap_out[3]));
     return 0;

@@ -1,8 +1,8 @@
-"""CPU stand-in for boojum_amd.sharded.HipShardOps, built on the oracle -- TEST ONLY.
+"""CPU steps of the sharded-commit model (tests/sharded_model.py), built on the oracle -- TEST ONLY.
 
-Lets the multi-process (gloo) tests exercise the sharded orchestration (column shards,
-all-gather order, leaf-range ownership, cap assembly incl. cap < G) on CPU tensors.
-Each step restates the same contract as the C-ABI entry point it stands in for
+Lets the multi-process (gloo) tests exercise the schedule of the native collective commit
+(column shards, exchange order, leaf-range ownership, cap assembly incl. cap < G) on CPU
+tensors.  Each step restates the contract of the C-ABI entry point the native call uses
 (include/boojum_mi355x.h: bj_lde_coeffs_d, bj_lde_shard_d, bj_lde_fold_shards_d,
 bj_lde_shard_folded_d, bj_merkle_*_d)."""
 import numpy as np
@@ -35,12 +35,14 @@ class CpuShardOps:
         br = int(O.bitreverse(np.arange(1 << log_shards, dtype=np.uint64))[shard])
         return O.gl_mul(O.gl_pow(O.domain_generator(log_n + log_lde), br), 7)
 
-    def fold_shards(self, coeffs, log_n, log_lde, log_shards, out):
-        # h_t = sum_a c_{t+am} (s_P^m)^a for every shard P; stored bit-reversed like the input
+    def fold_shards(self, coeffs, log_n, log_lde, log_shards, out, shards=None):
+        # h_t = sum_a c_{t+am} (s_P^m)^a for every listed shard P (default all), out[i] for
+        # shards[i]; stored bit-reversed like the input
         n = 1 << log_n
         m = (n << log_lde) >> log_shards
         f = n // m
-        for P in range(1 << log_shards):
+        shards = list(range(1 << log_shards)) if shards is None else list(shards)
+        for i, P in enumerate(shards):
             z = O.gl_pow(self._shard_shift(log_n, log_lde, log_shards, P), m)
             for c in range(coeffs.shape[0]):
                 mono = [int(x) for x in O.bitreverse(_np(coeffs)[c])]
@@ -51,7 +53,7 @@ class CpuShardOps:
                         zp = O.gl_mul(zp, z)
                         acc = O.gl_add(acc, O.gl_mul(mono[t + a * m], zp))
                     h.append(acc)
-                _np(out)[P, c] = O.bitreverse(np.array(h, dtype=np.uint64))
+                _np(out)[i, c] = O.bitreverse(np.array(h, dtype=np.uint64))
 
     def lde_shard_folded(self, folded, log_n, log_lde, log_shards, shard, lde):
         sp = self._shard_shift(log_n, log_lde, log_shards, shard)

@@ -24,16 +24,18 @@ def run_and_check(world, cfg, tmp_path, device):
     mp.start_processes(shard_worker.run, args=(world, free_port(), cfg, str(tmp_path), device, PATHS), nprocs=world,
                        join=True, start_method="spawn")
     n_cols, log_n, log_lde, cap = cfg[:4]
-    n, nl = 1 << log_n, 1 << (log_n + log_lde)
+    hasher = cfg[6] if len(cfg) > 6 and cfg[6] else "poseidon2"
+    log_k = cfg[7] if len(cfg) > 7 and cfg[7] is not None else log_lde
+    n, nd, nl = 1 << log_n, 1 << (log_n + log_lde), 1 << (log_n + log_k)
     m = nl // world
-    hasher = cfg[6] if len(cfg) > 6 else "poseidon2"
     if hasher == "poseidon2":
-        ref = O.lde_commit(O.synthetic_trace(n_cols, log_n), log_lde, cap, threads=4)
+        ref = O.lde_commit(O.synthetic_trace(n_cols, log_n), log_lde, cap, threads=4, log_k=log_k)
     else:
         _, lde = O.lde(O.synthetic_trace(n_cols, log_n), log_lde, threads=4)
-        leaves, nodes, _, cap_ref = O.merkle_construct(lde.reshape(n_cols, nl), cap, threads=4, hasher=hasher)
+        leaves, nodes, _, cap_ref = O.merkle_construct(np.ascontiguousarray(lde.reshape(n_cols, nd)[:, :nl]), cap,
+                                                       threads=4, hasher=hasher)
         ref = {"lde": lde, "leaves": leaves, "nodes": nodes, "cap": cap_ref}
-    lde_flat = ref["lde"].reshape(n_cols, nl)
+    lde_flat = ref["lde"].reshape(n_cols, nd)
     # global node levels: level k (k >= 1) holds nl >> k digests
     offs, o = [], 0
     k = 1
@@ -43,7 +45,10 @@ def run_and_check(world, cfg, tmp_path, device):
         k += 1
     for P in range(world):
         r = np.load(os.path.join(str(tmp_path), "rank%d.npz" % P))
-        assert np.array_equal(r["lde"], lde_flat[:, P * m:(P + 1) * m]), "rank %d lde" % P
+        # block j of rank P: range j G + P of the D-coset domain (cosets [j k, (j+1) k))
+        for j in range(nd // nl):
+            lo = j * nl + P * m
+            assert np.array_equal(r["lde"][j], lde_flat[:, lo:lo + m]), "rank %d lde block %d" % (P, j)
         assert np.array_equal(r["leaves"], ref["leaves"][P * m:(P + 1) * m]), "rank %d leaves" % P
         assert np.array_equal(r["cap"], ref["cap"]), "rank %d cap" % P
         # local subtree level k == slice of global level k

@@ -27,14 +27,16 @@ def test_c_caller_links_the_product_library():
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("log_n,cols,log_lde,cap,threads", [
-    (16, 32, 1, 16, 8),    # C1, seam called from 8 threads
-    (12, 19, 2, 8, 3),     # ragged leaf length (19 = 2 sponge blocks + 3)
-    (10, 8, 3, 32, 1),     # LDE x8, cap 32
+@pytest.mark.parametrize("log_n,cols,log_lde,cap,threads,log_k", [
+    (16, 32, 1, 16, 8, 1),    # C1, seam called from 8 threads
+    (12, 19, 2, 8, 3, 2),     # ragged leaf length (19 = 2 sponge blocks + 3)
+    (10, 8, 3, 32, 1, 3),     # LDE x8, cap 32
+    (14, 16, 3, 32, 4, 1),    # proof.json's shape ratio: LDE x8 (quotient degree), 2 cosets committed, cap 32
+    (13, 16, 2, 16, 2, 0),    # LDE x4, one coset committed (G = 8 > D: the sender-side fold)
 ])
-def test_c_caller(log_n, cols, log_lde, cap, threads):
+def test_c_caller(log_n, cols, log_lde, cap, threads, log_k):
     _need_bin()
-    r = subprocess.run([BIN, str(log_n), str(cols), str(log_lde), str(cap), str(threads)], capture_output=True,
-                       text=True, timeout=120)
+    r = subprocess.run([BIN, str(log_n), str(cols), str(log_lde), str(cap), str(threads), str(log_k)],
+                       capture_output=True, text=True, timeout=120)
     assert r.returncode == 0, r.stdout + r.stderr
     assert "c_caller ok" in r.stdout, r.stdout

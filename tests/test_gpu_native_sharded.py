@@ -6,7 +6,6 @@ sponge continuation, subtree, cap gather) with device-to-device copies in place 
 Every rank's LDE slice, leaves, subtree levels and cap must equal the oracle's single-process
 commit, bit for bit.  The RCCL transport itself is exercised at world 1 here (one GPU per rank
 is needed beyond that; bench.py --native runs it at N > 1)."""
-import ctypes
 import threading
 
 import numpy as np
@@ -26,22 +25,26 @@ def torch_mod():
     return torch
 
 
-def reference(n_cols, log_n, log_lde, cap, hasher):
+def reference(n_cols, log_n, log_lde, cap, hasher, log_k=None):
+    """The oracle's commit: LDE at D (flat (C, n D)), tree over the first k cosets."""
+    log_k = log_lde if log_k is None else log_k
     x = O.synthetic_trace(n_cols, log_n)
-    nl = 1 << (log_n + log_lde)
+    nd, nl = 1 << (log_n + log_lde), 1 << (log_n + log_k)
     if hasher == "poseidon2":
-        ref = O.lde_commit(x, log_lde, cap, threads=8)
+        ref = O.lde_commit(x, log_lde, cap, threads=8, log_k=log_k)
     else:
         _, lde = O.lde(x, log_lde, threads=8)
-        leaves, nodes, _, cap_ref = O.merkle_construct(lde.reshape(n_cols, nl), cap, threads=8, hasher=hasher)
+        leaves, nodes, _, cap_ref = O.merkle_construct(np.ascontiguousarray(lde.reshape(n_cols, nd)[:, :nl]), cap,
+                                                       threads=8, hasher=hasher)
         ref = {"lde": lde, "leaves": leaves, "nodes": nodes, "cap": cap_ref}
-    ref["lde"] = ref["lde"].reshape(n_cols, nl)
+    ref["lde"] = ref["lde"].reshape(n_cols, nd)
+    ref["nl"] = nl
     return ref
 
 
 def check_queries(ref, cap, qs, hasher):
     """OracleQuery::construct results (every rank the same) against the full tree's proofs."""
-    nl = ref["lde"].shape[1]
+    nl = ref["nl"]
     levels = (nl.bit_length() - 1) - (cap.bit_length() - 1)
     for idx, (elems, leaf, proof) in zip(query_indices(nl), qs):
         want_leaf, want_path = O.merkle_get_proof(ref["leaves"], ref["nodes"], levels, idx)
@@ -54,9 +57,13 @@ def check_queries(ref, cap, qs, hasher):
 def check_rank(ref, P, world, cap, lde, leaves, nodes, cap_got, qs=None, hasher="poseidon2"):
     if qs is not None:
         check_queries(ref, cap, qs, hasher)
-    nl = ref["lde"].shape[1]
+    nl, nd = ref["nl"], ref["lde"].shape[1]
     m = nl // world
-    assert np.array_equal(lde, ref["lde"][:, P * m:(P + 1) * m]), "rank %d lde" % P
+    # lde (B, C, m): block j is range j G + P of the D-coset domain (cosets [j k, (j+1) k))
+    assert lde.shape[0] == nd // nl
+    for j in range(nd // nl):
+        lo = j * nl + P * m
+        assert np.array_equal(lde[j], ref["lde"][:, lo:lo + m]), "rank %d lde block %d" % (P, j)
     assert np.array_equal(leaves, ref["leaves"][P * m:(P + 1) * m]), "rank %d leaves" % P
     assert np.array_equal(cap_got, ref["cap"]), "rank %d cap" % P
     # local subtree level k is the P-th slice of global level k
@@ -79,7 +86,7 @@ def query_indices(nl):
     return sorted({0, 1, nl // 2 - 1, nl // 2, nl - 1, (nl * 3) // 7})
 
 
-def run_local(torch, world, n_cols, log_n, log_lde, cap, hasher):
+def run_local(torch, world, n_cols, log_n, log_lde, cap, hasher, log_k=None):
     from boojum_amd._lib import call
     from boojum_amd.field import stream_of, to_host
     from boojum_amd.sharded import LocalGroup, native_columns, native_sharded_commit, native_sharded_query
@@ -98,10 +105,11 @@ def run_local(torch, world, n_cols, log_n, log_lde, cap, hasher):
                 cols = torch.tensor(native_columns(n_cols, world, P, hasher), device="cuda")
                 shard = trace.index_select(0, cols).contiguous()
                 comm = group.comm(P)
-                r = native_sharded_commit(comm, shard, n_cols, log_n, log_lde, cap, hasher)
+                r = native_sharded_commit(comm, shard, n_cols, log_n, log_lde, cap, hasher, log_commit_cosets=log_k)
                 s.synchronize()
-                qs = [native_sharded_query(comm, r, n_cols, log_n, log_lde, cap, i, hasher)
-                      for i in query_indices(1 << (log_n + log_lde))]
+                lk = log_lde if log_k is None else log_k
+                qs = [native_sharded_query(comm, r, n_cols, log_n, log_lde, cap, i, hasher, log_commit_cosets=log_k)
+                      for i in query_indices(1 << (log_n + lk))]
                 outs[P] = tuple(to_host(t) for t in (r.lde, r.leaves, r.nodes, r.cap)) + (qs,)
                 comm.close()
         except Exception as e:  # noqa: BLE001 - reported below
@@ -130,11 +138,20 @@ def run_local(torch, world, n_cols, log_n, log_lde, cap, hasher):
     (2, (16, 13, 2, 16, "blake2s")),     # chaining value carried across chunks
     (8, (16, 13, 1, 4, "blake2s")),
     (4, (16, 13, 1, 8, "keccak256")),    # no continuation: one chunk
+    # LDE at D, tree over the first k < D cosets (prover.rs:313-347, subset_for_degree)
+    (1, (16, 13, 3, 32, "poseidon2", 1)),   # proof.json's ratio: D = 8, k = 2, cap 32
+    (2, (16, 13, 3, 32, "poseidon2", 1)),   # G = k: whole cosets of every block
+    (4, (16, 13, 3, 32, "poseidon2", 1)),   # k < G <= D: sub-cosets folded at the receiver
+    (8, (16, 13, 3, 32, "poseidon2", 1)),   # G = D
+    (4, (16, 13, 2, 16, "poseidon2", 0)),   # D = 4, k = 1
+    (8, (16, 13, 2, 4, "poseidon2", 0)),    # G > D: sender-side fold per block, cap < G
+    (8, (16, 13, 2, 16, "blake2s", 0)),
 ])
 def test_native_sharded_commit_local_ranks(torch_mod, world, cfg):
-    n_cols, log_n, log_lde, cap, hasher = cfg
-    outs = run_local(torch_mod, world, n_cols, log_n, log_lde, cap, hasher)
-    ref = reference(n_cols, log_n, log_lde, cap, hasher)
+    n_cols, log_n, log_lde, cap, hasher = cfg[:5]
+    log_k = cfg[5] if len(cfg) > 5 else None
+    outs = run_local(torch_mod, world, n_cols, log_n, log_lde, cap, hasher, log_k)
+    ref = reference(n_cols, log_n, log_lde, cap, hasher, log_k)
     for P in range(world):
         check_rank(ref, P, world, cap, *outs[P], hasher=hasher)
 
@@ -142,14 +159,11 @@ def test_native_sharded_commit_local_ranks(torch_mod, world, cfg):
 def test_native_sharded_commit_rccl_world1(torch_mod):
     """The RCCL transport end to end at world 1 (ncclCommInitRank with one rank)."""
     torch = torch_mod
-    from boojum_amd._lib import call, check, load
+    from boojum_amd._lib import call
     from boojum_amd.field import stream_of, to_host
     from boojum_amd.sharded import NativeComm, native_sharded_commit
     n_cols, log_n, log_lde, cap = 16, 13, 2, 16
-    L = load()
-    uid = (ctypes.c_uint8 * 128)()
-    check(L.bj_comm_rccl_unique_id(uid), "unique id")
-    comm = NativeComm._make("bj_comm_init_rccl", uid, 1, 0, world=1, rank=0)
+    comm = NativeComm.rccl_world1()
     try:
         trace = torch.empty((n_cols, 1 << log_n), dtype=torch.int64, device="cuda")
         call("bj_fill_synthetic_d", trace.data_ptr(), n_cols, 1 << log_n, log_n, 42, 0, stream_of(trace))
@@ -212,7 +226,7 @@ def test_native_sharded_commit_c3_full_size(torch_mod, world):
                 r = native_sharded_commit(comm, shard, n_cols, log_n, log_lde, cap)
                 s.synchronize()
                 del shard
-                results[P] = (bool(torch.equal(r.lde, flat[:, P * m:(P + 1) * m])),
+                results[P] = (bool(torch.equal(r.lde[0], flat[:, P * m:(P + 1) * m])),
                               bool(torch.equal(r.leaves, ws.leaves[P * m:(P + 1) * m])),
                               bool(torch.equal(r.cap, ws.cap)))
                 del r
@@ -232,4 +246,95 @@ def test_native_sharded_commit_c3_full_size(torch_mod, world):
         assert lde_ok and leaves_ok and cap_ok, "rank %d of %d: lde %s leaves %s cap %s" % (
             P, world, lde_ok, leaves_ok, cap_ok)
     del ws, flat, trace
+    torch.cuda.empty_cache()
+
+
+def test_native_sharded_commit_peer_failure_aborts_group(torch_mod):
+    """A rank that rejects its arguments aborts the in-process group: its peer returns an error
+    instead of waiting forever at the first exchange (the group is unusable afterwards)."""
+    torch = torch_mod
+    from boojum_amd._lib import BoojumError
+    from boojum_amd.sharded import LocalGroup, native_sharded_commit
+    group = LocalGroup(2)
+    res = [None, None]
+
+    def rank_main(P):
+        torch.cuda.set_device(0)
+        comm = group.comm(P)
+        try:
+            shard = torch.zeros((8, 1 << 13), dtype=torch.int64, device="cuda")
+            native_sharded_commit(comm, shard, 16, 13, 1, 16 if P == 0 else 3)   # rank 1: cap not 2^k
+            torch.cuda.synchronize()
+            res[P] = "ok"
+        except BoojumError as e:
+            res[P] = str(e)
+        finally:
+            comm.close()
+
+    threads = [threading.Thread(target=rank_main, args=(P,), daemon=True) for P in range(2)]
+    for t in threads:
+        t.start()
+    for t in threads:
+        t.join(timeout=60)
+    assert not any(t.is_alive() for t in threads), "a rank is still blocked"
+    group.close()
+    assert "power-of-two" in res[1], res
+    assert "peer rank" in res[0], res
+
+
+@pytest.mark.slow
+def test_native_sharded_commit_c4_one_coset_per_rank(torch_mod):
+    """C4's intended split (BASELINE configs[3]): 2^23 x 256 at LDE x8 over G = D = 8 ranks, one
+    coset per rank, coefficients all-gathered.  Eight ranks do not fit one card at once (16 GiB
+    of gathered coefficients + 16 GiB of LDE each), so each rank runs alone through the native
+    call with a replay transport: its chunk all-gathers deliver the coefficient columns the
+    other ranks would have sent (bj_lde_coeffs_d format, taken from the one-GPU commit's
+    monomials), everything else -- its own iNTTs, its coset's LDE, the chained sponge, its
+    subtree -- is the product path.  Every rank's LDE, leaves and subtree root pair must equal
+    the one-GPU commit's slice, compared on the device."""
+    import ctypes
+    torch = torch_mod
+    from boojum_amd import commit
+    from boojum_amd._lib import EXCHANGE_FN
+    from boojum_amd.sharded import NativeComm, NativeShardedResult, native_columns, native_sharded_commit
+    n_cols, log_n, log_lde, cap = 256, 23, 3, 16
+    world, n = 8, 1 << 23
+    torch.cuda.empty_cache()
+    trace = commit.synthetic_trace(n_cols, log_n)
+    ws = commit.witness_commit(trace, 1 << log_lde, cap)
+    torch.cuda.synchronize()
+    hip = ctypes.CDLL("libamdhip64.so")
+    hip.hipMemcpyAsync.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_size_t, ctypes.c_int, ctypes.c_void_p]
+    mono = ws.scratch  # (C, n): the monomials in bj_lde_coeffs_d's bit-reversed format
+    cap_local = cap // world
+    for P in range(world):
+        state = {"base": None}
+
+        def replay(user, kind, send, recv, nbytes, stream, P=P, state=state):
+            assert kind == 0, "G = D exchanges by all-gather"
+            if nbytes < 8 * n:   # the cap gather: every rank's cap slice
+                src = ws.cap.data_ptr()
+                return hip.hipMemcpyAsync(recv, src, world * nbytes, 3, stream)
+            if state["base"] is None:
+                state["base"] = recv   # chunk 0 starts at column 0
+            c0 = (recv - state["base"]) // (8 * n)
+            return hip.hipMemcpyAsync(recv, mono[c0].data_ptr(), world * nbytes, 3, stream)
+
+        fn = EXCHANGE_FN(replay)
+        comm = NativeComm._make("bj_comm_init_callback", world, P, fn, None, 0, world=world, rank=P, keep=fn)
+        try:
+            cols = torch.tensor(native_columns(n_cols, world, P), device="cuda")
+            shard = trace.index_select(0, cols).contiguous()
+            res = NativeShardedResult(n_cols, log_n, log_lde, cap, world)
+            native_sharded_commit(comm, shard, n_cols, log_n, log_lde, cap, out=res)
+            torch.cuda.synchronize()
+            assert torch.equal(res.lde[0], ws.lde[:, P, :]), "rank %d lde (coset %d)" % (P, P)
+            assert torch.equal(res.leaves, ws.leaves[P * n:(P + 1) * n]), "rank %d leaves" % P
+            assert torch.equal(res.nodes[-cap_local:], ws.cap[P * cap_local:(P + 1) * cap_local]), \
+                "rank %d subtree roots" % P
+            del shard, res
+        finally:
+            comm.close()
+        torch.cuda.empty_cache()
+    del ws, trace, mono
     torch.cuda.empty_cache()

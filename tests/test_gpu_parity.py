@@ -347,35 +347,43 @@ def test_fri_base_oracle_leaves_from_fixture_on_gpu(bj):
 
 # --------------------------------------------------------------- commit
 
-@pytest.mark.parametrize("c,log_n,log_d,cap", [(32, 16, 1, 16), (7, 10, 2, 8), (9, 9, 3, 16), (1, 4, 1, 2)])
-def test_witness_commit_matches_oracle(bj, c, log_n, log_d, cap):
-    """Config 1 (2^16 x 32, LDE 2, cap 16) end to end, plus ragged shapes."""
+@pytest.mark.parametrize("c,log_n,log_d,cap,log_k", [
+    (32, 16, 1, 16, 1), (7, 10, 2, 8, 2), (9, 9, 3, 16, 3), (1, 4, 1, 2, 1),
+    # LDE at D, tree over the first k < D cosets through one call (prover.rs:313-347)
+    (16, 14, 3, 32, 1),   # proof.json's ratio: D = 8 (quotient degree), k = 2 (fri_lde_factor), cap 32
+    (12, 13, 2, 16, 0),   # D = 4, k = 1
+])
+def test_witness_commit_matches_oracle(bj, c, log_n, log_d, cap, log_k):
+    """Config 1 (2^16 x 32, LDE 2, cap 16) end to end, plus ragged shapes and k < D."""
     tr_np = O.synthetic_trace(c, log_n)
     tr = bj.commit.synthetic_trace(c, log_n)
     eq(bj.field.to_host(tr), tr_np)
-    ws = bj.commit.witness_commit(tr, 1 << log_d, cap)
-    ref = O.lde_commit(tr_np, log_d, cap, threads=8)
+    ws = bj.commit.witness_commit(tr, 1 << log_d, cap, fri_lde_factor=1 << log_k)
+    ref = O.lde_commit(tr_np, log_d, cap, threads=8, log_k=log_k)
     eq(bj.field.to_host(ws.lde), ref["lde"])
     eq(bj.field.to_host(ws.leaves), ref["leaves"])
     eq(bj.field.to_host(ws.nodes), ref["nodes"])
     eq(bj.field.to_host(ws.cap), ref["cap"])
 
 
-@pytest.mark.parametrize("c,log_n,log_d,cap", [(5, 8, 2, 4), (70, 10, 1, 16), (64, 12, 2, 8), (33, 14, 3, 16)])
-def test_commit_host_abi_matches(bj, c, log_n, log_d, cap):
+@pytest.mark.parametrize("c,log_n,log_d,cap,log_k", [(5, 8, 2, 4, 2), (70, 10, 1, 16, 1), (64, 12, 2, 8, 2),
+                                                     (33, 14, 3, 16, 3), (40, 14, 3, 32, 1), (20, 12, 2, 16, 0)])
+def test_commit_host_abi_matches(bj, c, log_n, log_d, cap, log_k):
     """bj_lde_commit_h: the column-chunked host pipeline (32-column chunks: one ragged, several
-    full, and a 1-column tail) equals the oracle's one-shot commit."""
+    full, and a 1-column tail) equals the oracle's one-shot commit, also with the tree over the
+    first k < D cosets (D = 8 / k = 2 / cap 32, proof.json's ratio; D = 4 / k = 1)."""
     import ctypes
     from boojum_amd._lib import call
     tr = O.synthetic_trace(c, log_n)
-    nl = 1 << (log_n + log_d)
+    nl = 1 << (log_n + log_k)
     lde = np.zeros((c, 1 << log_d, 1 << log_n), dtype=np.uint64)
     leaves = np.zeros((nl, 4), dtype=np.uint64)
     nodes = np.zeros((nl - cap, 4), dtype=np.uint64)
     capo = np.zeros((cap, 4), dtype=np.uint64)
     p = lambda a: a.ctypes.data_as(ctypes.POINTER(ctypes.c_uint64))  # noqa: E731
-    call("bj_lde_commit_h", p(np.ascontiguousarray(tr)), c, log_n, log_d, cap, p(lde), p(leaves), p(nodes), p(capo))
-    ref = O.lde_commit(tr, log_d, cap, threads=8)
+    call("bj_lde_commit_h", p(np.ascontiguousarray(tr)), c, log_n, log_d, log_k, cap, p(lde), p(leaves), p(nodes),
+         p(capo))
+    ref = O.lde_commit(tr, log_d, cap, threads=8, log_k=log_k)
     eq(lde, ref["lde"])
     eq(leaves, ref["leaves"])
     eq(nodes, ref["nodes"])

@@ -1,8 +1,9 @@
-"""The RCCL (backend "nccl") calls of the sharded commit, on a one-rank group on the one GPU of
-the box: the in-place all-gather and the all-to-all of boojum_amd/sharded.py with async handles
-ordering the compute stream, under the bench's process-group options (high-priority stream).
-A one-rank group cannot show bandwidth or overlap; it checks that the calls, options and
-stream ordering the 8-GPU run depends on are accepted by this torch/RCCL build."""
+"""The bench's N > 1 communicator path on the one GPU of the box: a torch.distributed "nccl"
+(RCCL) process group of one rank with the bench's options (high-priority stream), and
+NativeComm.rccl over it (rank 0 makes the RCCL unique id, the group broadcasts it,
+ncclCommInitRank) driving bj_sharded_commit_d.  A one-rank group cannot show bandwidth or
+overlap; it checks that the calls the 8-GPU run depends on are accepted by this torch/RCCL
+build and give the one-GPU commit."""
 
 import pytest
 
@@ -24,28 +25,20 @@ def pg(tmp_path_factory):
     dist.destroy_process_group()
 
 
-def test_all_gather_in_place_and_all_to_all(pg):
+@pytest.mark.parametrize("log_lde,log_k", [(2, 2), (3, 1)])
+def test_native_commit_over_process_group_comm(pg, log_lde, log_k):
     torch = pg
-    from boojum_amd import sharded
-    buf = torch.arange(64, dtype=torch.int64, device="cuda").reshape(8, 8)
-    src = buf[2:4].clone()
-    h = sharded._all_gather(buf[2:4], buf[2:4], async_op=True)   # in place, one rank
-    h.wait()
-    assert torch.equal(buf[2:4], src)
-    out = torch.empty((4, 8), dtype=torch.int64, device="cuda")
-    inp = torch.arange(32, dtype=torch.int64, device="cuda").reshape(4, 8) * 3
-    h = sharded._all_to_all(out, inp, async_op=True)
-    h.wait()
-    y = out + 1                     # ordered after the collective on the current stream
-    torch.cuda.synchronize()
-    assert torch.equal(y, inp + 1)
-
-
-def test_cap_all_gather_sync(pg):
-    torch = pg
-    from boojum_amd import sharded
-    cap = torch.empty((4, 4), dtype=torch.int64, device="cuda")
-    local = torch.arange(16, dtype=torch.int64, device="cuda").reshape(4, 4)
-    sharded._all_gather(cap, local)
-    torch.cuda.synchronize()
-    assert torch.equal(cap, local)
+    from boojum_amd import commit
+    from boojum_amd.sharded import NativeComm, native_sharded_commit
+    n_cols, log_n, cap = 16, 13, 16
+    comm = NativeComm.rccl()
+    try:
+        trace = commit.synthetic_trace(n_cols, log_n)
+        r = native_sharded_commit(comm, trace, n_cols, log_n, log_lde, cap, log_commit_cosets=log_k)
+        ws = commit.witness_commit(trace, 1 << log_lde, cap, fri_lde_factor=1 << log_k)
+        torch.cuda.synchronize()
+        nd = (1 << log_n) << log_lde
+        assert torch.equal(r.lde.permute(1, 0, 2).reshape(n_cols, nd), ws.lde.view(n_cols, nd))
+        assert torch.equal(r.leaves, ws.leaves) and torch.equal(r.nodes, ws.nodes) and torch.equal(r.cap, ws.cap)
+    finally:
+        comm.close()

@@ -1,5 +1,6 @@
 """GPU parity of the coset-sharded LDE (bj_lde_coeffs_d / bj_lde_shard_d) and of the
-multi-rank sharded commit on one card (gloo staging; RCCL needs one GPU per rank).
+multi-process sharded commit on one card: the native collective (bj_sharded_commit_d) in G
+processes joined by a gloo group through the callback transport (RCCL needs one GPU per rank).
 
 Each shard's LDE must equal the matching leaf range of the oracle's full LDE, bit for bit,
 for G <= D (whole cosets), G > D (folded sub-cosets, F = G/D up to 8) and sizes on both the
@@ -88,10 +89,13 @@ def test_lde_shard_errors(torch_mod):
         call("bj_lde_shard_folded_d", None, 1, 8, 4, 1, 2, 4, None, None)    # shard >= G
 
 
-@pytest.mark.parametrize("world,cfg", [(2, (8, 10, 1, 16)), (4, (8, 9, 1, 2)), (2, (48, 10, 2, 16, 1)),
-                                       (4, (64, 12, 1, 4, 1)), (8, (64, 9, 1, 16)), (2, (256, 9, 1, 16)),
-                                       (4, (64, 12, 1, 4, 1, False)), (8, (128, 14, 2, 16)),
-                                       (4, (64, 12, 1, 4, 1, None, "blake2s")), (2, (32, 10, 1, 16, 0, None, "keccak256"))])
-def test_sharded_commit_multirank_one_gpu(torch_mod, world, cfg, tmp_path):
+@pytest.mark.parametrize("world,cfg", [(2, (8, 10, 1, 16)), (4, (8, 9, 1, 2)), (2, (48, 10, 2, 16)),
+                                       (4, (64, 12, 1, 4)), (8, (64, 9, 1, 16)), (2, (256, 9, 1, 16)),
+                                       (8, (128, 14, 2, 16)),
+                                       (4, (64, 12, 1, 4, 0, None, "blake2s")),
+                                       (2, (32, 10, 1, 16, 0, None, "keccak256")),
+                                       (4, (32, 12, 3, 32, 0, None, None, 1)),     # D = 8, k = 2, cap 32
+                                       (8, (32, 12, 2, 16, 0, None, None, 0))])    # D = 4, k = 1, G > D
+def test_sharded_commit_multiprocess_one_gpu(torch_mod, world, cfg, tmp_path):
     from sharded_check import run_and_check
     run_and_check(world, cfg, tmp_path, "cuda")

@@ -1,10 +1,11 @@
 """Host logic of the native collective commit (no GPU): bj_sharded_columns deals the trace
-columns exactly as the Python orchestration (ShardedWorkspace.my_columns) does, and rejects
-the shapes the reference's asserts reject."""
+columns exactly as the CPU model of its schedule (tests/sharded_model.py, which the gloo tests
+check against the oracle) does, and rejects the shapes the reference's asserts reject."""
 import pytest
 
 from boojum_amd._lib import BoojumError
-from boojum_amd.sharded import ShardedWorkspace, native_columns
+from boojum_amd.sharded import native_columns
+from sharded_model import ShardModel
 from shard_cpu_ops import CpuShardOps
 
 
@@ -14,7 +15,7 @@ from shard_cpu_ops import CpuShardOps
 def test_native_deal_matches_python_orchestration(n_cols, world, hasher):
     seen = []
     for rank in range(world):
-        ws = ShardedWorkspace(n_cols, 4, 1, 2, rank, world, device="cpu", ops=CpuShardOps(hasher), hasher=hasher)
+        ws = ShardModel(n_cols, 4, 1, 2, rank, world, CpuShardOps(hasher), hasher=hasher)
         cols = native_columns(n_cols, world, rank, hasher)
         assert cols == ws.my_columns, (n_cols, world, rank, hasher)
         seen += cols

@@ -29,7 +29,7 @@ def main():
     leaves = np.empty((nl, 4), dtype=np.uint64)
     nodes = np.empty((nl - cap, 4), dtype=np.uint64)
     capo = np.empty((cap, 4), dtype=np.uint64)
-    args = (tr.ctypes.data_as(p), c, log_n, log_d, cap, lde.ctypes.data_as(p), leaves.ctypes.data_as(p),
+    args = (tr.ctypes.data_as(p), c, log_n, log_d, log_d, cap, lde.ctypes.data_as(p), leaves.ctypes.data_as(p),
             nodes.ctypes.data_as(p), capo.ctypes.data_as(p))
     pinned = len(sys.argv) > 4 and sys.argv[4] == "pinned"
     if pinned:

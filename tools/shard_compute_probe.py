@@ -1,11 +1,13 @@
 #!/usr/bin/env python3
-"""Per-rank compute of the G-way sharded commit, measured on one GPU with the exchange
-stubbed out: rank P's LDE range, leaves and subtree for G = 1, 2, 4, 8 at C3.  The result
-bounds the multi-GPU step time from below (exchange fully hidden).  It is not a bench
-line (the coefficient buffer holds this rank's own columns only, so the values are not a
-real commit).
+"""Per-rank compute of the G-way sharded commit, measured on one GPU with the exchange stubbed
+out: rank 0 runs the native collective call (bj_sharded_commit_d) over a transport whose
+exchanges move nothing (NativeComm.null), so the time is its iNTTs (+ folds), its LDE range,
+leaves and subtree alone.  The result bounds the multi-GPU step time from below (exchange fully
+hidden).  It is not a bench line: the received buffers are never filled, so the values are not
+a commitment.
 
-usage: python tools/shard_compute_probe.py [config]
+usage: python tools/shard_compute_probe.py [config ...]      (default: C3 at G = 1, 2, 4, 8 and
+                                                               C4 at G = 8, one coset per rank)
 """
 import json
 import os
@@ -19,83 +21,43 @@ sys.path.insert(0, ROOT)
 def main():
     import torch
     import bench
-    from boojum_amd import sharded
-    cfg = sys.argv[1] if len(sys.argv) > 1 else "C3"
-    n_cols, log_n, log_lde, cap = bench.CONFIGS[cfg]
+    from boojum_amd._lib import call
+    from boojum_amd.field import stream_of
+    from boojum_amd.sharded import NativeComm, NativeShardedResult, native_columns, native_sharded_commit
+    plan = [("C3", 1), ("C3", 2), ("C3", 4), ("C3", 8), ("C4", 8)]
+    if len(sys.argv) > 1:
+        plan = [(c, w) for c, w in plan if c in sys.argv[1:]]
     out = {}
-
-    def compute(ws, tr):
-        """sharded_witness_commit without its collectives (rank 0's compute only)."""
-        ops = ws.ops
-        for k, (lo, g, c) in enumerate(ws.column_runs()):
-            if ws.fold_exchange:
-                ops.coeffs(tr[lo:lo + c], ws.own[lo:lo + c], ws.log_n)
-                ops.fold_shards(ws.own[lo:lo + c], ws.log_n, ws.log_lde, ws.log_g, ws.send_chunk(lo, c))
-            else:
-                ops.coeffs(tr[lo:lo + c], ws.coeffs[g:g + c], ws.log_n)
-        for k in range(ws.n_chunks):
-            c0, c1 = ws.chunk_columns(k)
-            if ws.fold_exchange:
-                ops.lde_shard_folded(ws.folded[c0:c1], ws.log_n, ws.log_lde, ws.log_g, ws.rank, ws.lde[c0:c1])
-            else:
-                work = None if ws.work is None else ws.work[:c1 - c0]
-                ops.lde_shard(ws.coeffs[c0:c1], ws.log_n, ws.log_lde, ws.log_g, ws.rank, work, ws.lde[c0:c1])
-            last = k == ws.n_chunks - 1
-            ops.leaves(ws.lde[c0:c1], ws.leaves if last else ws.state, cap_in=None if k == 0 else ws.state,
-                       final=last)
-        ops.nodes(ws.leaves, ws.cap_local, ws.nodes)
-
-    class TimedOps:
-        """Wraps the ops object: events around every call, summed per op name."""
-
-        def __init__(self, inner):
-            self.inner, self.ev = inner, []
-
-        def __getattr__(self, name):
-            fn = getattr(self.inner, name)
-            if not callable(fn):
-                return fn
-
-            def run(*a, **k):
-                s, e = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-                s.record()
-                r = fn(*a, **k)
-                e.record()
-                self.ev.append((name, s, e))
-                return r
-            return run
-
-        def totals(self, reps):
-            torch.cuda.synchronize()
-            acc = {}
-            for name, s, e in self.ev:
-                acc[name] = acc.get(name, 0.0) + s.elapsed_time(e)
-            return {k: round(v / reps, 3) for k, v in acc.items()}
-
-    runs = [(w, True) for w in (1, 2, 4, 8)] + [(w, False) for w in (8,) if w > (1 << log_lde)]
-    for world, fold in runs:
-        ws = sharded.ShardedWorkspace(n_cols, log_n, log_lde, cap, 0, world, device="cuda", fold_exchange=fold)
-        tr = ws.synthetic_trace_shard()
-        compute(ws, tr)   # warm-up
+    for cfg, world in plan:
+        n_cols, log_n, log_lde, cap = bench.CONFIGS[cfg]
+        n = 1 << log_n
+        comm = NativeComm.null(world, 0) if world > 1 else NativeComm.rccl_world1()
+        tr = torch.empty((n_cols // world, n), dtype=torch.int64, device="cuda")
+        for j, c in enumerate(native_columns(n_cols, world, 0)):
+            call("bj_fill_synthetic_d", tr[j].data_ptr(), 1, n, log_n, 42, c, stream_of(tr))
+        res = NativeShardedResult(n_cols, log_n, log_lde, cap, world)
+        native_sharded_commit(comm, tr, n_cols, log_n, log_lde, cap, out=res)   # warm-up
         torch.cuda.synchronize()
         s, e = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        reps = 3
         s.record()
-        for _ in range(3):
-            compute(ws, tr)
+        for _ in range(reps):
+            native_sharded_commit(comm, tr, n_cols, log_n, log_lde, cap, out=res)
         e.record()
         torch.cuda.synchronize()
-        ms = s.elapsed_time(e) / 3
-        timed = TimedOps(ws.ops)
-        ws.ops = timed
-        compute(ws, tr)
-        phases = timed.totals(1)
-        ws.ops = timed.inner
-        out["%d%s" % (world, "" if fold or world <= (1 << log_lde) else "_allgather")] = {
-            "ms_per_rank": round(ms, 2), "chunks": ws.n_chunks,
-            "ideal_elems_per_s": n_cols * (1 << log_n) / (ms * 1e-3), "phase_ms": phases}
-        del ws, tr
+        ms = s.elapsed_time(e) / reps
+        out["%s_G%d" % (cfg, world)] = {
+            "ms_per_rank": round(ms, 2), "ideal_elems_per_s": n_cols * n / (ms * 1e-3),
+            "exchange": "none" if world == 1 else ("all-to-all (sender fold)" if world > (1 << log_lde)
+                                                   else "all-gather"),
+            "received_bytes_per_rank": 0 if world == 1 else (
+                8 * n_cols * ((n << log_lde) // world) * (world - 1) // world if world > (1 << log_lde)
+                else 8 * n * n_cols * (world - 1) // world)}
+        print(json.dumps({cfg + "_G%d" % world: out["%s_G%d" % (cfg, world)]}), flush=True)
+        comm.close()
+        del tr, res
         torch.cuda.empty_cache()
-    print(json.dumps({"config": cfg, "per_rank_compute": out}))
+    print(json.dumps({"per_rank_compute": out}))
 
 
 if __name__ == "__main__":
