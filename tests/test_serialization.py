@@ -79,3 +79,35 @@ def test_serde_json_is_canonical_and_compact():
     assert S.dumps(q) == '{"leaf_elements":[0,5,3],"proof":[[0,1,2,3],[4,5,6,7]]}'
     with pytest.raises(ValueError):
         S.cap_from_json([[1, 2, 3]])
+
+
+def test_byte_digest_tree_layout_blake2s():
+    """MerkleTreeWithCap<F, Blake2s256>: H::Output = [u8; 32], so leaf hashes and node levels go
+    out as Vec<[u8; 32]> (fast_serialization.rs:343-358): the length prefix counts BYTES (32 per
+    digest) and the payload is the raw digest bytes -- here the 4 little-endian words of each."""
+    import hashlib
+    digests = [hashlib.blake2s(bytes([i])).digest() for i in range(6)]
+    words = np.frombuffer(b"".join(digests), dtype="<u8").astype(np.uint64).reshape(6, 4)
+    t = _Tree(2, words[:4], [words[4:]])
+    t.hasher = "blake2s"
+    f = io.BytesIO()
+    S.write_merkle_tree(f, t)
+    want = le(2) + le(128) + b"".join(digests[:4]) + le(1) + le(64) + b"".join(digests[4:])
+    assert f.getvalue() == want
+    f.seek(0)
+    cap, lv, levels = S.read_merkle_tree(f, "blake2s")
+    assert cap == 2 and np.array_equal(lv, words[:4]) and np.array_equal(levels[0], words[4:])
+
+
+def test_byte_digest_json_is_raw_bytes():
+    """serde writes a [u8; 32] digest as 32 integers: no reduction mod p (a word >= p survives)."""
+    w = np.array([[0xFFFFFFFFFFFFFFFF, 1, 2, 0xFFFFFFFF00000001]], dtype=np.uint64)
+    j = S.cap_to_json(w, "keccak256")
+    assert len(j) == 1 and len(j[0]) == 32 and j[0][:8] == [255] * 8 and j[0][8] == 1
+    assert np.array_equal(S.cap_from_json(j, "keccak256"), w)
+    q = S.oracle_query_to_json(np.array([5, 0xFFFFFFFF00000002], dtype=np.uint64), w, "blake2s")
+    assert q["leaf_elements"] == [5, 1] and len(q["proof"][0]) == 32
+    leaf, proof = S.oracle_query_from_json(q, "blake2s")
+    assert np.array_equal(proof, w)
+    with pytest.raises(ValueError):
+        S.cap_to_json(w, "sha256")
