@@ -1,0 +1,31 @@
+"""The golden caps bench.py verifies against (tests/golden/bench_caps.json,
+tools/make_bench_golden.py) are the oracle's caps of the bench configs' synthetic traces:
+recompute the small ones here."""
+import json
+import os
+
+import numpy as np
+import pytest
+
+import oracle as O
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+@pytest.mark.parametrize("key,cfg", [("C1/poseidon2", (32, 16, 1, 16)), ("C5/poseidon2", (93, 16, 3, 16))])
+def test_golden_caps_are_the_oracle_caps(key, cfg):
+    g = json.load(open(os.path.join(ROOT, "tests", "golden", "bench_caps.json")))["caps"]
+    assert "C3/poseidon2" in g, "the headline config's golden cap is missing"
+    n_cols, log_n, log_lde, cap = cfg
+    ref = O.lde_commit(O.synthetic_trace(n_cols, log_n), log_lde, cap, threads=os.cpu_count() or 1)
+    want = [["%016x" % int(x) for x in row] for row in ref["cap"].astype(np.uint64)]
+    assert g[key]["cap"] == want
+
+
+def test_bench_reads_the_golden_cap():
+    import sys
+    sys.path.insert(0, ROOT)
+    import bench
+    c3 = bench.golden_cap("C3", "poseidon2")
+    assert c3 is not None and len(c3) == 16 and all(len(d) == 4 for d in c3)
+    assert bench.golden_cap("C3", "keccak256") is None

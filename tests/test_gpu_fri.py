@@ -63,3 +63,35 @@ def test_folding_schedule_keeps_low_degree(bj):
     for w in (w0, w1):
         mono = O.ifft_natural_to_natural(O.bitreverse(w), O.gl_inv(ci))
         assert not mono[len(mono) >> log_d:].any()
+
+
+def test_gpu_fold_reproduces_proof_json_fri_chain(bj):
+    """bj_fri_fold_d on the reference's own FRI data: for the first six queries of proof.json,
+    every committed FRI leaf (8 Ext2 values) folded three times by 2 on the GPU -- with the
+    transcript-derived challenges (oracle/transcript.py replays the verifier's Poseidon2
+    transcript), the full-domain inverse twiddles at the leaf's flat pair indices and the coset
+    inverse of that step -- equals the value the next oracle commits, and the last step's equals
+    final_fri_monomials at the folded point (verifier.rs:2396-2518)."""
+    import json
+    import os
+    import transcript as T
+    torch = bj.torch
+    fx = json.load(open(os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden", "proof_fri.json")))
+    rep = T.replay(fx)
+    n = fx["vk"]["domain_size"] * fx["proof_config"]["fri_lde_factor"]
+    roots = bj.fri.precompute_roots(n)
+    for q in rep["queries"]:
+        steps = q["steps"]
+        for k, st in enumerate(steps):
+            leaf = [int(v) for v in st["leaf"]]
+            deg = len(leaf) // 2
+            c0 = bj.field.to_device(np.array(leaf[:deg], dtype=np.uint64))
+            c1 = bj.field.to_device(np.array(leaf[deg:], dtype=np.uint64))
+            base, ci = st["tree_idx"] * deg // 2, st["coset_inverse"]
+            for ch in st["challenges"]:
+                c0, c1 = bj.fri.fold(c0, c1, roots[base:], ci, ch)
+                base //= 2
+                ci = ci * ci % O.P
+            got = (int(bj.field.to_host(c0)[0]), int(bj.field.to_host(c1)[0]))
+            want = steps[k + 1]["expected"] if k + 1 < len(steps) else q["final"]
+            assert got == want, "query %d step %d" % (q["index"], k)
