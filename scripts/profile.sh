@@ -1,6 +1,7 @@
 #!/bin/bash
 # rocprofv3 evidence for the C3 bench: the default bench line (with the CPU baseline), a
-# kernel-trace stats run, then one PMC pass per counter group.
+# kernel-trace stats run, one PMC pass per counter group, the FETCH_SIZE / WRITE_SIZE
+# calibration on known byte counts (tools/fetch_calibration.hip), and the per-rank compute probe.
 # usage: bash scripts/profile.sh TAG
 set -u
 TAG=${1:-r2}
@@ -19,3 +20,9 @@ timeout -s KILL 240 rocprofv3 --pmc WRITE_SIZE --output-format csv -d $OUT/write
 echo write ok
 timeout -s KILL 240 rocprofv3 --pmc SQ_INSTS_VALU SQ_WAVES SQ_BUSY_CYCLES SQ_WAVE_CYCLES SQ_ACTIVE_INST_VALU GRBM_GUI_ACTIVE --output-format csv -d $OUT/sq -o run -- $B --steps 1 --warmup 0 > $OUT/sq.log 2>&1 || { echo "sq rc=$?"; tail -5 $OUT/sq.log; exit 1; }
 echo sq ok
+timeout -s KILL 60 rocprofv3 --pmc FETCH_SIZE --output-format csv -d $OUT/cal_fetch -o run -- ./tools/fetch_calibration > $OUT/cal_fetch.log 2>&1 || { echo "cal fetch rc=$?"; tail -5 $OUT/cal_fetch.log; exit 1; }
+timeout -s KILL 60 rocprofv3 --pmc WRITE_SIZE --output-format csv -d $OUT/cal_write -o run -- ./tools/fetch_calibration > $OUT/cal_write.log 2>&1 || { echo "cal write rc=$?"; tail -5 $OUT/cal_write.log; exit 1; }
+echo calibration ok
+timeout -k 10 300 python3 tools/shard_compute_probe.py > $OUT/shard_compute.log 2>&1 || { echo "probe rc=$?"; tail -5 $OUT/shard_compute.log; exit 1; }
+tail -1 $OUT/shard_compute.log
+echo done

@@ -7,13 +7,12 @@ counter per kernel over its dispatches and writes profiles/pmc_summary.json:
 
 Units and gfx950 corrections (MI355X_MICROARCH.md, HBM section):
 * FETCH_SIZE and WRITE_SIZE are in KiB.
-* FETCH_SIZE reports half the bytes of a wide contiguous stream. That holds for the leaf kernel and the NTT tails
-  (512 contiguous bytes per wave load; leaf: FETCH_SIZE = 16 GiB against its known 32 GiB of reads;
-  tails: the inverse + forward average 10.1 GiB against a known 20 GiB).
-  The NTT heads read 128-byte runs. The DIF heads' FETCH_SIZE equalled their known byte count
-  (iNTT head: 8 GiB), so they are not doubled; the CT heads (other grid order) report half of
-  it (iNTT head: 4.3 GB against 8 GiB), so they are.
-The per-kernel factor is the third field of KERNELS; each was calibrated on a known byte count.
+* FETCH_SIZE reports half the bytes of every read shape these kernels use, calibrated
+  independently of them on known byte counts (tools/fetch_calibration.hip, 2 GiB each,
+  profiles/r2a_fetch_calibration.json): 8-byte-per-lane column loads (the leaf kernel's and the
+  NTT tails' shape) 0.5000, 128-byte runs of 8-byte lanes (the NTT heads' strided rows) 0.5000,
+  16-byte-per-lane streams 0.5000.  WRITE_SIZE equals the bytes of 8-byte-per-lane stores
+  (1.0000).  So every read is doubled (the third field of KERNELS) and writes are taken as is.
 
 usage: python tools/pmc_summary.py gpurun_out/prof_TAG [--config C3]
 """
@@ -33,8 +32,8 @@ KERNELS = [
     ("bj::(anonymous namespace)::ct_head_kernel<9, 1", "ct_head_fwd", 2.0),
     ("bj::(anonymous namespace)::ct_head_kernel<9, 0", "ct_head_inv", 2.0),
     ("bj::(anonymous namespace)::ct_tail_kernel", "ct_tail", 2.0),
-    ("bj::(anonymous namespace)::dif_head_kernel<9, 1>", "dif_head_fwd", 1.0),
-    ("bj::(anonymous namespace)::dif_head_kernel<9, 0>", "dif_head_inv", 1.0),
+    ("bj::(anonymous namespace)::dif_head_kernel<9, 1>", "dif_head_fwd", 2.0),
+    ("bj::(anonymous namespace)::dif_head_kernel<9, 0>", "dif_head_inv", 2.0),
     ("bj::(anonymous namespace)::dif_tail_kernel", "dif_tail", 2.0),
 ]
 
