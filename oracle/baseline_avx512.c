@@ -1,12 +1,12 @@
 /*
- * AVX-512 leaf hashing for the CPU BASELINE leg of bench.py -- test/bench infrastructure, not
- * the checker and not product code.
+ * AVX-512 leaf hashing and LDE for the CPU BASELINE leg of bench.py -- test/bench
+ * infrastructure, not the checker and not product code.
  *
  * The reference selects its AVX-512 field and Poseidon2 paths on an AVX-512 host
  * (field/goldilocks/mod.rs:36-75, avx512_impl.rs:357-428, poseidon2/state_avx512.rs) when built
  * with -C target-cpu=native, as its bench scripts do.  The scalar C restatement (boojum_oracle.c)
- * would understate that CPU, so the baseline's leaf hashing -- 80% of its time -- runs here on
- * 8 leaves per 512-bit vector: the same permutation (poseidon2_permutation,
+ * would understate that CPU, so the baseline's leaf hashing runs here on 8 leaves per 512-bit
+ * vector (and its LDE on 8 butterflies per vector, below): the same permutation (poseidon2_permutation,
  * state_generic_impl.rs:221-236; MDS suggested_mds.rs:19-97; M_I :166-202) and sponge
  * (Overwrite, zero padding, sponge.rs:224-323), lane i hashing leaf L + i.  The Goldilocks
  * multiply is the 4 x 32x32 product + reduction of avx512_impl.rs:357-428 (mod.rs:186-199).
@@ -195,5 +195,156 @@ int bjo_merkle_leaves_avx512(const u64* src, size_t col_stride, uint32_t n_cols,
     for (int t = 0; t < nt; t++) pthread_join(th[t], NULL);
     free(th);
     free(jobs);
+    return 0;
+}
+
+/* ------------------------------------------------------------------ LDE (baseline) */
+/* The baseline's coset LDE (transform_raw_storages_to_lde, utils.rs:270-403) with the CT
+ * butterflies of serial_ct_ntt_natural_to_bitreversed (fft/mod.rs:659-734) run 8 pairs per
+ * vector wherever a group has >= 8 pairs (the MixedGL path's idea, fft/mod.rs:852-1077); the
+ * last three stages, the bit reversal and the twiddle tables stay scalar.  Same values as
+ * bjo_lde (checked in tests/test_oracle_baseline.py). */
+void bjo_precompute_twiddles(uint32_t log_n, int inverse, u64* out);
+void bjo_bitreverse_inplace(u64* a, size_t n);
+void bjo_lde_cosets(uint32_t log_n, uint32_t log_d, u64* out);
+u64 bjo_gl_mul(u64 a, u64 b);
+u64 bjo_gl_inv(u64 a);
+
+AVX512 static inline __m512i vsub(__m512i a, __m512i b) {
+    const __m512i eps = _mm512_set1_epi64((long long)EPS);
+    __m512i d = _mm512_sub_epi64(a, b);
+    __mmask8 b1 = _mm512_cmplt_epu64_mask(a, b);
+    __m512i t = _mm512_mask_sub_epi64(d, b1, d, eps);
+    __mmask8 b2 = b1 & _mm512_cmplt_epu64_mask(d, eps);
+    return _mm512_mask_sub_epi64(t, b2, t, eps);
+}
+
+static inline u64 s_add(u64 a, u64 b) {
+    u64 s = a + b;
+    if (s < a) { u64 t = s + EPS; if (t < s) t += EPS; s = t; }
+    return s;
+}
+static inline u64 s_sub(u64 a, u64 b) {
+    u64 d = a - b;
+    if (a < b) { u64 t = d - EPS; if (d < EPS) t -= EPS; d = t; }
+    return d;
+}
+
+AVX512 static void vct_ntt(u64* a, size_t n, const u64* tw) {
+    if (n == 1) return;
+    size_t pairs = n / 2, groups = 1;
+    while (groups < n) {
+        for (size_t k = 0; k < groups; k++) {
+            u64* lo = a + k * pairs * 2;
+            u64* hi = lo + pairs;
+            const u64 s = k == 0 ? 1 : tw[k];   /* the first stage's twiddle is 1 (:678-699) */
+            if (pairs >= 8) {
+                const __m512i w = _mm512_set1_epi64((long long)s);
+                for (size_t j = 0; j < pairs; j += 8) {
+                    __m512i u = _mm512_loadu_si512((const void*)(lo + j));
+                    __m512i v = _mm512_loadu_si512((const void*)(hi + j));
+                    if (groups > 1) v = vmul(v, w);
+                    _mm512_storeu_si512((void*)(hi + j), vsub(u, v));
+                    _mm512_storeu_si512((void*)(lo + j), vadd(u, v));
+                }
+            } else {
+                for (size_t j = 0; j < pairs; j++) {
+                    u64 u = lo[j], v = groups > 1 ? bjo_gl_mul(hi[j], s) : hi[j];
+                    hi[j] = s_sub(u, v);
+                    lo[j] = s_add(u, v);
+                }
+            }
+        }
+        pairs /= 2;
+        groups *= 2;
+    }
+}
+
+/* x[i] *= scale * e^i */
+AVX512 static void vdistribute(u64* a, size_t n, u64 e, u64 scale) {
+    if (n < 8) {
+        u64 s = scale;
+        for (size_t i = 0; i < n; i++) { a[i] = bjo_gl_mul(a[i], s); s = bjo_gl_mul(s, e); }
+        return;
+    }
+    u64 p[8];
+    p[0] = scale;
+    for (int i = 1; i < 8; i++) p[i] = bjo_gl_mul(p[i - 1], e);
+    __m512i pw = _mm512_loadu_si512((const void*)p);
+    const __m512i step = _mm512_set1_epi64((long long)bjo_gl_mul(bjo_gl_mul(bjo_gl_mul(e, e), bjo_gl_mul(e, e)),
+                                                                  bjo_gl_mul(bjo_gl_mul(e, e), bjo_gl_mul(e, e))));
+    for (size_t i = 0; i < n; i += 8) {
+        _mm512_storeu_si512((void*)(a + i), vmul(_mm512_loadu_si512((const void*)(a + i)), pw));
+        pw = vmul(pw, step);
+    }
+}
+
+AVX512 static void vcanon_all(u64* a, size_t n) {
+    size_t i = 0;
+    for (; i + 8 <= n; i += 8) _mm512_storeu_si512((void*)(a + i), vcanon(_mm512_loadu_si512((const void*)(a + i))));
+    for (; i < n; i++) if (a[i] >= 0xFFFFFFFF00000001ull) a[i] -= 0xFFFFFFFF00000001ull;
+}
+
+typedef struct {
+    u64* cols; size_t n; const u64* tw; u64* lde; uint32_t n_cols, d; const u64* cosets;
+    int phase; size_t begin, end;
+} vlde_t;
+
+AVX512 static void* vlde_run(void* p) {
+    vlde_t* x = (vlde_t*)p;
+    for (size_t job = x->begin; job < x->end; job++) {
+        if (x->phase == 0) {
+            /* ifft_natural_to_natural (fft/mod.rs:464-491): CT with inverse twiddles, bit
+             * reversal, times n^-1 */
+            u64* c = x->cols + job * x->n;
+            vct_ntt(c, x->n, x->tw);
+            bjo_bitreverse_inplace(c, x->n);
+            if (x->n > 1) vdistribute(c, x->n, 1, bjo_gl_inv((u64)x->n));
+            vcanon_all(c, x->n);
+        } else {
+            /* fft_natural_to_bitreversed with coset i (utils.rs:355-379 job order) */
+            size_t coset = job / x->n_cols, col = job % x->n_cols;
+            u64* dst = x->lde + (col * x->d + coset) * x->n;
+            memcpy(dst, x->cols + col * x->n, x->n * sizeof(u64));
+            vdistribute(dst, x->n, x->cosets[coset], 1);
+            vct_ntt(dst, x->n, x->tw);
+            vcanon_all(dst, x->n);
+        }
+    }
+    return NULL;
+}
+
+static void vscope(int threads, size_t work, vlde_t* proto) {
+    if (threads < 1) threads = 1;
+    size_t chunk = (work + threads - 1) / threads;
+    int nt = chunk ? (int)((work + chunk - 1) / chunk) : 0;
+    pthread_t* th = (pthread_t*)malloc(sizeof(pthread_t) * (nt ? nt : 1));
+    vlde_t* jobs = (vlde_t*)malloc(sizeof(vlde_t) * (nt ? nt : 1));
+    for (int t = 0; t < nt; t++) {
+        jobs[t] = *proto;
+        jobs[t].begin = t * chunk;
+        jobs[t].end = (t + 1) * chunk < work ? (t + 1) * chunk : work;
+        pthread_create(&th[t], NULL, vlde_run, &jobs[t]);
+    }
+    for (int t = 0; t < nt; t++) pthread_join(th[t], NULL);
+    free(th);
+    free(jobs);
+}
+
+/* As bjo_lde (trace overwritten with the monomials; lde n_cols x D x n); -1 without AVX-512. */
+int bjo_lde_avx512(u64* trace, uint32_t n_cols, uint32_t log_n, uint32_t log_d, u64* lde, int threads) {
+    if (!bjo_avx512_available()) return -1;
+    size_t n = (size_t)1 << log_n, d = (size_t)1 << log_d;
+    u64* tw = (u64*)malloc(sizeof(u64) * (n / 2 > 0 ? n / 2 : 1));
+    u64* cosets = (u64*)malloc(sizeof(u64) * d);
+    bjo_lde_cosets(log_n, log_d, cosets);
+    vlde_t x = {trace, n, tw, lde, n_cols, (uint32_t)d, cosets, 0, 0, 0};
+    if (n >= 2) bjo_precompute_twiddles(log_n, 1, tw);
+    vscope(threads, n_cols, &x);
+    if (n >= 2) bjo_precompute_twiddles(log_n, 0, tw);
+    x.phase = 1;
+    vscope(threads, (size_t)n_cols * d, &x);
+    free(tw);
+    free(cosets);
     return 0;
 }

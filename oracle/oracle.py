@@ -61,6 +61,12 @@ def lib():
         L.bjo_keccak_leaf.argtypes = [_u64p, sz, _u64p]
         L.bjo_keccak_node.argtypes = [_u64p, _u64p, _u64p]
         L.bjo_merkle_leaves_with.argtypes = [_u64p, sz, u32, sz, _u64p, i, i]
+        L.bjo_avx512_available.restype = i
+        L.bjo_avx512_available.argtypes = []
+        L.bjo_lde_avx512.restype = i
+        L.bjo_lde_avx512.argtypes = [_u64p, u32, u32, u32, _u64p, i]
+        L.bjo_merkle_leaves_avx512.restype = i
+        L.bjo_merkle_leaves_avx512.argtypes = [_u64p, sz, u32, sz, _u64p, i]
         L.bjo_merkle_nodes_with.restype = i
         L.bjo_merkle_nodes_with.argtypes = [_u64p, sz, u32, _u64p, i, i]
         L.bjo_merkle_construct_with.restype = i
@@ -274,9 +280,37 @@ def merkle_construct(lde_flat, cap_size, threads=1, hasher="poseidon2"):
     return leaves, nodes[:n_nodes], levels, cap
 
 
-def merkle_construct_timed(lde_flat, cap_size, threads=1, hasher="poseidon2"):
+def lde_avx512(trace, log_d, threads=1):
+    """The CPU baseline's AVX-512 LDE (oracle/baseline_avx512.c): same values as lde().  None when
+    the host has no AVX-512."""
+    tr = _u64(trace).copy()
+    c, n = tr.shape
+    log_n = n.bit_length() - 1
+    out = np.zeros((c, 1 << log_d, n), dtype=np.uint64)
+    if lib().bjo_lde_avx512(_p(tr), c, log_n, log_d, _p(out), threads) != 0:
+        return None
+    return tr, out
+
+
+def avx512_available():
+    return bool(lib().bjo_avx512_available())
+
+
+def merkle_leaves_avx512(lde_flat, threads=1):
+    """The CPU baseline's 8-leaf AVX-512 Poseidon2 leaf hashing (oracle/baseline_avx512.c):
+    same leaves as merkle_construct's.  None when the host has no AVX-512."""
+    src = _u64(lde_flat)
+    c, nl = src.shape
+    leaves = np.zeros((nl, 4), dtype=np.uint64)
+    if lib().bjo_merkle_leaves_avx512(_p(src), nl, c, nl, _p(leaves), threads) != 0:
+        return None
+    return leaves
+
+
+def merkle_construct_timed(lde_flat, cap_size, threads=1, hasher="poseidon2", simd=False):
     """merkle_construct with the reference's own phase split (merkle_tree.rs:162-167 leaf timing,
-    :438-442 node timing): returns (leaves, nodes, levels, cap, {"leaves": s, "nodes": s})."""
+    :438-442 node timing): returns (leaves, nodes, levels, cap, {"leaves": s, "nodes": s}).
+    simd: hash the leaves with the AVX-512 baseline path (Poseidon2, host permitting)."""
     import time
     src = _u64(lde_flat)
     c, nl = src.shape
@@ -285,7 +319,9 @@ def merkle_construct_timed(lde_flat, cap_size, threads=1, hasher="poseidon2"):
     n_nodes = nl - cap_size if levels > 0 else 0
     nodes = np.zeros((max(n_nodes, 1), 4), dtype=np.uint64)
     t0 = time.perf_counter()
-    lib().bjo_merkle_leaves_with(_p(src), nl, c, nl, _p(leaves), threads, HASHERS[hasher])
+    if not (simd and hasher == "poseidon2" and nl % 8 == 0 and
+            lib().bjo_merkle_leaves_avx512(_p(src), nl, c, nl, _p(leaves), threads) == 0):
+        lib().bjo_merkle_leaves_with(_p(src), nl, c, nl, _p(leaves), threads, HASHERS[hasher])
     t1 = time.perf_counter()
     got = lib().bjo_merkle_nodes_with(_p(leaves), nl, cap_size, _p(nodes), threads, HASHERS[hasher])
     t2 = time.perf_counter()
