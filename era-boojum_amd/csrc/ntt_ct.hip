@@ -364,9 +364,12 @@ __device__ __forceinline__ void tw_ct_tailC(uint64_t* w, const uint64_t* __restr
     for (int p = 0; p < 16; p++) w[p] = base[pair_lo(p, HK) >> (13 - V)];
 }
 
+// CANON: canonicalise the output (a template parameter: a run-time branch per element made the
+// compiler wait on each epilogue LDS read separately).
+template <bool CANON>
 __global__ __launch_bounds__(NT, 2) void ct_tail_kernel(uint64_t* dst, size_t dst_col_stride, size_t coset_stride,
                                                         uint32_t log_n, const uint64_t* __restrict__ tab,
-                                                        size_t tab_stride, int canon_out) {
+                                                        size_t tab_stride) {
     __shared__ uint64_t lds[PAD_LDS];
     const uint32_t t = threadIdx.x;
     const size_t q = blockIdx.y;
@@ -422,7 +425,7 @@ __global__ __launch_bounds__(NT, 2) void ct_tail_kernel(uint64_t* dst, size_t ds
 #pragma unroll
     for (int k = 0; k < PT; k++) {
         const uint64_t v = lds[ba + tail_off_a(k)];
-        d[t + NT * k] = canon_out ? canon_u64(v) : v;
+        d[t + NT * k] = CANON ? canon_u64(v) : v;
     }
 }
 
@@ -533,8 +536,12 @@ hipError_t launch_ct(uint64_t* dst, size_t dst_col_stride, size_t coset_stride, 
         case 9: launch_head_R<9>(mode, k_on, g, dst, dst_col_stride, coset_stride, src, src_stride, log_n, tab, tab_stride, kappa, st); break;
         default: launch_head_R<10>(mode, k_on, g, dst, dst_col_stride, coset_stride, src, src_stride, log_n, tab, tab_stride, kappa, st); break;
     }
-    hipLaunchKernelGGL(ct_tail_kernel, g, dim3(NT), 0, st, dst, dst_col_stride, coset_stride, log_n, tab, tab_stride,
-                       canon_out ? 1 : 0);
+    if (canon_out)
+        hipLaunchKernelGGL(ct_tail_kernel<true>, g, dim3(NT), 0, st, dst, dst_col_stride, coset_stride, log_n, tab,
+                           tab_stride);
+    else
+        hipLaunchKernelGGL(ct_tail_kernel<false>, g, dim3(NT), 0, st, dst, dst_col_stride, coset_stride, log_n, tab,
+                           tab_stride);
     return hipGetLastError();
 }
 

@@ -629,6 +629,52 @@ void bjo_merkle_leaves_with(const u64* lde, size_t col_stride, uint32_t n_cols, 
     worker_scope(threads, n_leaves, leaf_job, &x);
 }
 
+/* The same leaves absorbed over a column range (the sponge is sequential over the row's
+ * elements, sponge.rs:224-239): cap_in holds the 4 capacity words per leaf after the columns
+ * before this range (NULL: fresh sponge); n_cols must be a multiple of 8 unless final, so the
+ * range starts and ends on a rate boundary.  final == 0: out = capacity words (state[8..12))
+ * after this range; final != 0: out = the leaf digests as bjo_merkle_leaves_with.  Lets a
+ * caller hash a trace too large to hold whole, a column chunk at a time. */
+typedef struct {
+    const u64* lde;
+    size_t col_stride;
+    uint32_t n_cols;
+    const u64* cap_in;
+    u64* out;
+    int final_;
+} lp_ctx_t;
+
+static void leaf_partial_job(void* c, size_t b, size_t e) {
+    lp_ctx_t* x = (lp_ctx_t*)c;
+    for (size_t L = b; L < e; L++) {
+        u64 s[12] = {0};
+        if (x->cap_in)
+            for (int i = 0; i < 4; i++) s[8 + i] = x->cap_in[4 * L + i];
+        size_t filled = 0;
+        for (uint32_t i = 0; i < x->n_cols; i++) {
+            s[filled++] = x->lde[(size_t)i * x->col_stride + L];
+            if (filled == 8) { bjo_poseidon2_permutation(s); filled = 0; }
+        }
+        if (x->final_) {
+            if (filled > 0) {
+                for (size_t i = filled; i < 8; i++) s[i] = 0;
+                bjo_poseidon2_permutation(s);
+            }
+            for (int i = 0; i < 4; i++) x->out[4 * L + i] = gl_canon(s[i]);
+        } else {
+            for (int i = 0; i < 4; i++) x->out[4 * L + i] = s[8 + i];
+        }
+    }
+}
+
+int bjo_poseidon2_leaves_partial(const u64* lde, size_t col_stride, uint32_t n_cols, size_t n_leaves,
+                                 const u64* cap_in, u64* out, int final_, int threads) {
+    if (!final_ && n_cols % 8 != 0) return -1;
+    lp_ctx_t x = {lde, col_stride, n_cols, cap_in, out, final_};
+    worker_scope(threads, n_leaves, leaf_partial_job, &x);
+    return 0;
+}
+
 /* ... and the node levels over them (continue_from_leaf_hashes, :388-449). */
 int bjo_merkle_nodes_with(const u64* leaves, size_t n_leaves, uint32_t cap_size, u64* nodes, int threads,
                           int hasher) {

@@ -73,6 +73,8 @@ def lib():
         L.bjo_merkle_construct_with.argtypes = [_u64p, sz, u32, sz, u32, _u64p, _u64p, i, i]
         L.bjo_verify_proof_over_cap_with.restype = i
         L.bjo_verify_proof_over_cap_with.argtypes = [_u64p, i, _u64p, _u64p, sz, i]
+        L.bjo_poseidon2_leaves_partial.restype = i
+        L.bjo_poseidon2_leaves_partial.argtypes = [_u64p, sz, u32, sz, _u64p, _u64p, i, i]
         L.bjo_find_query_index.restype = ctypes.c_long
         L.bjo_find_query_index.argtypes = [_u64p, _u64p, i, _u64p, sz]
         _LIB = L
@@ -376,6 +378,31 @@ def lde_commit(trace, log_d, cap_size, threads=1, log_k=None, in_place=False):
     lib().bjo_lde_commit_subset(_p(tr), c, log_n, log_d, log_k, cap_size, _p(lde_out), _p(leaves), _p(nodes),
                                 _p(cap), threads)
     return {"monomials": tr, "lde": lde_out, "leaves": leaves, "nodes": nodes[:n_nodes], "cap": cap}
+
+
+def poseidon2_leaves_partial(lde_cols, cap_in, final, threads=1):
+    """Leaf sponges over a column range (bjo_poseidon2_leaves_partial): lde_cols (C, N) the
+    range's columns in leaf order, cap_in (N, 4) the capacity words after the previous columns
+    or None.  final: (N, 4) digests; else (N, 4) capacity words to carry on."""
+    src = _u64(lde_cols)
+    c, nl = src.shape
+    out = np.zeros((nl, 4), dtype=np.uint64)
+    cin = None if cap_in is None else _u64(cap_in)
+    rc = lib().bjo_poseidon2_leaves_partial(_p(src), nl, c, nl, None if cin is None else _p(cin), _p(out),
+                                            1 if final else 0, threads)
+    if rc != 0:
+        raise ValueError("a non-final column range must be a multiple of 8 columns")
+    return out
+
+
+def merkle_nodes(leaves, cap_size, threads=1, hasher="poseidon2"):
+    """Node levels over given leaf digests (bjo_merkle_nodes_with); returns (nodes, cap)."""
+    lv = _u64(leaves).reshape(-1, 4)
+    nl = lv.shape[0]
+    nodes = np.zeros((max(nl - cap_size, 1), 4), dtype=np.uint64)
+    levels = lib().bjo_merkle_nodes_with(_p(lv), nl, cap_size, _p(nodes), threads, HASHERS[hasher])
+    cap = lv[:cap_size] if levels == 0 else nodes[nl - 2 * cap_size:nl - cap_size]
+    return nodes[:nl - cap_size], cap.copy()
 
 
 def find_query_index(leaf, path, cap):
