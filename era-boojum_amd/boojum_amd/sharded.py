@@ -142,6 +142,17 @@ class NativeComm:
         fn = _EXCHANGE_FN(lambda *a: 0)
         return cls._make("bj_comm_init_callback", world, rank, fn, None, 0, world=world, rank=rank, keep=fn)
 
+    def set_timing(self, on=True):
+        """Record phase events in every later bj_sharded_commit_d call (bj_comm_set_timing)."""
+        check(load().bj_comm_set_timing(self.handle, 1 if on else 0), "bj_comm_set_timing")
+
+    def phase_ms(self):
+        """Summed ms of the timed calls since the last read: ({inverse, lde, leaves, nodes}, calls)."""
+        ms = (ctypes.c_float * 4)()
+        calls = ctypes.c_int()
+        check(load().bj_comm_phase_ms(self.handle, ms, ctypes.byref(calls)), "bj_comm_phase_ms")
+        return dict(zip(("inverse", "lde", "leaves", "nodes"), list(ms))), calls.value
+
     def close(self):
         if self.handle:
             load().bj_comm_destroy(self.handle)

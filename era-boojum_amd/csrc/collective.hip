@@ -149,9 +149,45 @@ struct bj_comm {
     int host_staged = 1;
     hipStream_t xs = nullptr;  // exchange stream, high priority, created on first use
     int xs_dev = -1;
+    // bj_comm_set_timing: (start, end, phase) event triples of the calls not yet read
+    bool timing = false;
+    struct Interval {
+        hipEvent_t a, b;
+        int phase;
+    };
+    std::vector<Interval> intervals;
+    int timed_calls = 0;
 };
 
 namespace {
+
+// Phase intervals of one timed call (bj_comm_set_timing); a no-op when timing is off.
+struct PhaseTimer {
+    bj_comm* c;
+    hipStream_t st;
+    hipEvent_t open = nullptr;
+    int phase = -1;
+    PhaseTimer(bj_comm* comm, hipStream_t s) : c(comm), st(s) {}
+    int begin(int ph) {
+        if (!c->timing) return BJ_OK;
+        HIP_CHECK(hipEventCreate(&open), "hipEventCreate");
+        phase = ph;
+        HIP_CHECK(hipEventRecord(open, st), "hipEventRecord");
+        return BJ_OK;
+    }
+    int end() {
+        if (!c->timing || !open) return BJ_OK;
+        hipEvent_t e;
+        HIP_CHECK(hipEventCreate(&e), "hipEventCreate");
+        HIP_CHECK(hipEventRecord(e, st), "hipEventRecord");
+        c->intervals.push_back({open, e, phase});
+        open = nullptr;
+        return BJ_OK;
+    }
+    ~PhaseTimer() {
+        if (open) (void)hipEventDestroy(open);
+    }
+};
 
 int exchange_stream(bj_comm* c, hipStream_t* out) {
     int dev = 0;
@@ -465,8 +501,38 @@ int bj_comm_init_callback(int world, int rank, bj_exchange_fn fn, void* user, in
     return BJ_OK;
 }
 
+int bj_comm_set_timing(bj_comm* c, int on) {
+    if (!c) return err(BJ_EINVAL, "null communicator");
+    c->timing = on != 0;
+    return BJ_OK;
+}
+
+int bj_comm_phase_ms(bj_comm* c, float* ms_out4, int* calls_out) {
+    if (!c || !ms_out4) return err(BJ_EINVAL, "null argument");
+    float acc[4] = {0, 0, 0, 0};
+    int rc = BJ_OK;
+    for (const bj_comm::Interval& iv : c->intervals) {
+        float ms = 0;
+        hipError_t e = hipEventSynchronize(iv.b);
+        if (e == hipSuccess) e = hipEventElapsedTime(&ms, iv.a, iv.b);
+        if (e != hipSuccess && rc == BJ_OK) rc = err(BJ_EHIP, std::string("phase timing: ") + hipGetErrorString(e));
+        if (iv.phase >= 0 && iv.phase < 4) acc[iv.phase] += ms;
+        (void)hipEventDestroy(iv.a);
+        (void)hipEventDestroy(iv.b);
+    }
+    c->intervals.clear();
+    for (int i = 0; i < 4; i++) ms_out4[i] = acc[i];
+    if (calls_out) *calls_out = c->timed_calls;
+    c->timed_calls = 0;
+    return rc;
+}
+
 int bj_comm_destroy(bj_comm* c) {
     if (!c) return BJ_OK;
+    for (const bj_comm::Interval& iv : c->intervals) {
+        (void)hipEventDestroy(iv.a);
+        (void)hipEventDestroy(iv.b);
+    }
     int rc = BJ_OK;
     if (c->xs) (void)hipStreamDestroy(c->xs);
     if (c->kind == bj_comm::RCCL_OWNED && c->nccl) {
@@ -545,6 +611,8 @@ int bj_sharded_commit_d(bj_comm* comm, const uint64_t* trace_shard, size_t trace
         HIP_CHECK(arrived.make(K), "hipEventCreate");
     }
     std::vector<uint64_t> spm(world);
+    // phases 0 inverse (+ fold), 1 lde, 2 leaves, 3 nodes (bj_comm_set_timing)
+    PhaseTimer pt(comm, st);
 
     // 1. local inverse transforms (and folds), each chunk's exchange issued as soon as its
     //    part is ready
@@ -556,6 +624,7 @@ int bj_sharded_commit_d(bj_comm* comm, const uint64_t* trace_shard, size_t trace
             // send layout per run: [block j][rank p][c][m], so block j's all-to-all is contiguous
             uint64_t* snd = send + (size_t)world * B * m * r.lo;
             uint64_t* mine = own + (size_t)r.lo * n;
+            BJ_CHECK(pt.begin(0));
             BJ_CHECK(bj_lde_coeffs_d(tr, r.count, trace_stride, log_n, mine, n, st));
             for (uint32_t j = 0; j < B; j++) {
                 for (uint32_t p = 0; p < world; p++)
@@ -564,6 +633,7 @@ int bj_sharded_commit_d(bj_comm* comm, const uint64_t* trace_shard, size_t trace
                                               r.count, log2u(m), log_f, world, spm.data(), st),
                           "fold");
             }
+            BJ_CHECK(pt.end());
             if (world > 1) {
                 HIP_CHECK(hipEventRecord(in.ev[k], st), "hipEventRecord");
                 HIP_CHECK(hipStreamWaitEvent(xs, in.ev[k], 0), "hipStreamWaitEvent");
@@ -574,7 +644,9 @@ int bj_sharded_commit_d(bj_comm* comm, const uint64_t* trace_shard, size_t trace
             if (world > 1) HIP_CHECK(hipEventRecord(arrived.ev[k], xs), "hipEventRecord");
         } else {
             uint64_t* mine = coeffs + (size_t)r.global * n;
+            BJ_CHECK(pt.begin(0));
             BJ_CHECK(bj_lde_coeffs_d(tr, r.count, trace_stride, log_n, mine, n, st));
+            BJ_CHECK(pt.end());
             if (world > 1) {
                 HIP_CHECK(hipEventRecord(in.ev[k], st), "hipEventRecord");
                 HIP_CHECK(hipStreamWaitEvent(xs, in.ev[k], 0), "hipStreamWaitEvent");
@@ -592,25 +664,31 @@ int bj_sharded_commit_d(bj_comm* comm, const uint64_t* trace_shard, size_t trace
         for (uint32_t j = 0; j < B; j++) {
             uint64_t* out = lde + ((size_t)j * n_cols + r.c0) * m;
             const uint32_t shard = j * world + rank;
+            BJ_CHECK(pt.begin(1));
             if (fold)
                 BJ_CHECK(bj_lde_shard_folded_d(folded + ((size_t)j * n_cols + r.c0) * m, cc, m, log_n, log_lde, ls,
                                                shard, out, st));
             else
                 BJ_CHECK(bj_lde_shard_d(coeffs + (size_t)r.c0 * n, cc, n, log_n, log_lde, ls, shard, work, out, st));
+            BJ_CHECK(pt.end());
             if (j) continue;
             const bool last = k + 1 == K;
             const uint64_t* cin = k == 0 ? nullptr : state;
             uint64_t* dst = last ? leaves : state;
+            BJ_CHECK(pt.begin(2));
             if (hasher == BJ_HASHER_POSEIDON2)
                 BJ_CHECK(bj_merkle_leaves_partial_d(out, cc, m, m, cin, dst, last ? 1 : 0, st));
             else if (hasher == BJ_HASHER_BLAKE2S)
                 BJ_CHECK(bj_blake2s_leaves_partial_d(out, cc, m, m, r.c0, cin, dst, last ? 1 : 0, st));
             else
                 BJ_CHECK(bj_keccak256_leaves_d(out, cc, m, m, dst, st));
+            BJ_CHECK(pt.end());
         }
     }
     // 3. this rank's subtree, then the cap
+    BJ_CHECK(pt.begin(3));
     BJ_CHECK(nodes_for(hasher, leaves, m, cap_local, nodes, st));
+    BJ_CHECK(pt.end());
     const uint64_t* local_cap = nodes + (m - 2 * (size_t)cap_local) * 4;
     if (cap_size >= world) {
         BJ_CHECK(all_gather(comm, local_cap, cap, (size_t)cap_local * 32, st));
@@ -625,6 +703,7 @@ int bj_sharded_commit_d(bj_comm* comm, const uint64_t* trace_shard, size_t trace
                                  hipMemcpyDeviceToDevice, st),
                   "memcpy cap");
     }
+    if (comm->timing) comm->timed_calls++;
     xs_join.ok = abort_guard.ok = true;
     return BJ_OK;
 }

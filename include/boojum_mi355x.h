@@ -307,6 +307,15 @@ int bj_comm_local_group_destroy(void* group);
 int bj_comm_init_local(void* group, int rank, bj_comm** out);
 int bj_comm_init_callback(int world, int rank, bj_exchange_fn exchange, void* user, int host_staged, bj_comm** out);
 int bj_comm_destroy(bj_comm* comm);
+/* Phase timing of bj_sharded_commit_d on this communicator (no reference counterpart: the
+ * reference logs its phase times, merkle_tree.rs:162-167, prover.rs:345).  on != 0: every later
+ * call records HIP events on its compute stream around the inverse transforms (+ folds), the
+ * LDE evaluations, the leaf hashing and the subtree + cap; waits for the exchange are outside
+ * every interval.  bj_comm_phase_ms waits for the recorded calls, writes the summed
+ * milliseconds {inverse, lde, leaves, nodes} to ms_out[4] and their count to *calls_out, and
+ * starts a new sum. */
+int bj_comm_set_timing(bj_comm* comm, int on);
+int bj_comm_phase_ms(bj_comm* comm, float* ms_out4, int* calls_out);
 
 #define BJ_HASHER_POSEIDON2 0
 #define BJ_HASHER_BLAKE2S 1

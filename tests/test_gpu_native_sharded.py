@@ -175,6 +175,41 @@ def test_native_sharded_commit_rccl_world1(torch_mod):
         comm.close()
 
 
+def test_native_sharded_commit_phase_timing(torch_mod):
+    """bj_comm_set_timing / bj_comm_phase_ms: the timed calls give positive phase times that
+    fit inside the call, the count of calls, a fresh sum after each read, and the same
+    commitment as an untimed call."""
+    torch = torch_mod
+    from boojum_amd._lib import call
+    from boojum_amd.field import stream_of, to_host
+    from boojum_amd.sharded import NativeComm, native_sharded_commit
+    n_cols, log_n, log_lde, cap = 32, 14, 2, 16
+    comm = NativeComm.rccl_world1()
+    try:
+        trace = torch.empty((n_cols, 1 << log_n), dtype=torch.int64, device="cuda")
+        call("bj_fill_synthetic_d", trace.data_ptr(), n_cols, 1 << log_n, log_n, 42, 0, stream_of(trace))
+        plain = to_host(native_sharded_commit(comm, trace, n_cols, log_n, log_lde, cap).cap)
+        assert comm.phase_ms() == ({"inverse": 0.0, "lde": 0.0, "leaves": 0.0, "nodes": 0.0}, 0)
+        comm.set_timing(True)
+        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        e0.record()
+        for _ in range(2):
+            r = native_sharded_commit(comm, trace, n_cols, log_n, log_lde, cap)
+        e1.record()
+        torch.cuda.synchronize()
+        ms, calls = comm.phase_ms()
+        assert calls == 2 and all(v > 0 for v in ms.values())
+        assert sum(ms.values()) <= e0.elapsed_time(e1) * 1.05
+        assert (to_host(r.cap) == plain).all()
+        assert comm.phase_ms()[1] == 0
+        comm.set_timing(False)
+        native_sharded_commit(comm, trace, n_cols, log_n, log_lde, cap)
+        torch.cuda.synchronize()
+        assert comm.phase_ms()[1] == 0
+    finally:
+        comm.close()
+
+
 def test_native_sharded_commit_rejects_bad_shapes(torch_mod):
     torch = torch_mod
     from boojum_amd._lib import BoojumError

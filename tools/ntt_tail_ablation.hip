@@ -8,6 +8,8 @@
 //   3 no LDS exchanges     the three exchanges and their barriers removed
 //   4 no twiddle loads     twiddles from registers
 //   5 butterflies only     1 + 2 + 3 + 4
+//   6 nontemporal stores   the full kernel with streaming stores
+//   7 ... and loads        streaming loads and stores
 // Build: hipcc -O3 -std=c++17 --offload-arch=gfx950 -I era-boojum_amd/csrc -o tools/ntt_tail_ablation tools/ntt_tail_ablation.hip
 #include "../era-boojum_amd/csrc/ntt_ct.hip"
 #include <cstdio>
@@ -19,12 +21,12 @@ template <int ABL>
 __device__ __forceinline__ void tail_unit_body(uint64_t* lds, uint64_t* d, const uint64_t* __restrict__ ct, size_t q,
                                                uint32_t u0) {
     constexpr bool LOAD = ABL != 1 && ABL != 5, STORE = ABL != 2 && ABL != 5, EXCH = ABL != 3 && ABL != 5,
-                   TWL = ABL != 4 && ABL != 5;
+                   TWL = ABL != 4 && ABL != 5, NTS = ABL == 6 || ABL == 7, NTL = ABL == 7;
     const uint32_t t = threadIdx.x;
     uint64_t x[PT], wa[16], wb[16];
     if constexpr (LOAD) {
 #pragma unroll
-        for (int k = 0; k < PT; k++) x[k] = d[t + NT * k];
+        for (int k = 0; k < PT; k++) x[k] = NTL ? __builtin_nontemporal_load(d + t + NT * k) : d[t + NT * k];
     } else {
 #pragma unroll
         for (int k = 0; k < PT; k++) x[k] = (uint64_t)(t + 1) * (2 * k + 1) + q;
@@ -107,7 +109,10 @@ __device__ __forceinline__ void tail_unit_body(uint64_t* lds, uint64_t* d, const
     }
     if constexpr (STORE) {
 #pragma unroll
-        for (int k = 0; k < PT; k++) d[t + NT * k] = canon_u64(x[k]);
+        for (int k = 0; k < PT; k++) {
+            if constexpr (NTS) __builtin_nontemporal_store(canon_u64(x[k]), d + t + NT * k);
+            else d[t + NT * k] = canon_u64(x[k]);
+        }
     } else {
         uint64_t acc = 0;
 #pragma unroll
@@ -165,15 +170,16 @@ int main() {
     const dim3 g(cols, (unsigned)(n / bj::TILE), cosets);
     using K = void (*)(uint64_t*, size_t, size_t, uint32_t, const uint64_t*, size_t);
     const K ks[] = {bj::tail_ablation<0>, bj::tail_ablation<1>, bj::tail_ablation<2>,
-                    bj::tail_ablation<3>, bj::tail_ablation<4>, bj::tail_ablation<5>};
+                    bj::tail_ablation<3>, bj::tail_ablation<4>, bj::tail_ablation<5>,
+                    bj::tail_ablation<6>, bj::tail_ablation<7>};
     const char* names[] = {"full", "no global load", "no store", "no LDS exchanges", "no twiddle loads",
-                           "butterflies only"};
+                           "butterflies only", "nontemporal stores", "nontemporal loads and stores"};
     hipEvent_t a, b;
     CHECK(hipEventCreate(&a));
     CHECK(hipEventCreate(&b));
     int cus = 256;
     CHECK(hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, 0));
-    for (int mult = 2; mult <= 8; mult *= 2) {
+    for (int mult = 2; mult <= 2; mult *= 2) {
         const uint32_t units = g.x * g.y * g.z, blocks = cus * mult;
         hipLaunchKernelGGL(bj::tail_persistent, dim3(blocks), dim3(bj::NT), 0, 0, buf, n * cosets, n, log_n, tab, n,
                            g.x, g.y, units);
@@ -189,7 +195,7 @@ int main() {
         CHECK(hipEventElapsedTime(&ms, a, b));
         printf("{\"variant\": \"persistent %d blocks/CU\", \"ms\": %.3f}\n", mult, ms / 3);
     }
-    for (int v = 0; v < 6; v++) {
+    for (int v = 0; v < 8; v++) {
         hipLaunchKernelGGL(ks[v], g, dim3(bj::NT), 0, 0, buf, n * cosets, n, log_n, tab, n);
         CHECK(hipGetLastError());
         CHECK(hipDeviceSynchronize());
