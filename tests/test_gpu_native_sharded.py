@@ -326,7 +326,7 @@ def test_native_sharded_commit_c4_one_coset_per_rank(torch_mod):
     other ranks would have sent (bj_lde_coeffs_d format, taken from the one-GPU commit's
     monomials), everything else -- its own iNTTs, its coset's LDE, the chained sponge, its
     subtree -- is the product path.  Every rank's LDE, leaves and subtree root pair must equal
-    the one-GPU commit's slice, compared on the device."""
+    the one-GPU commit's slice, compared on the device; that commit's cap equals the oracle's."""
     import ctypes
     torch = torch_mod
     from boojum_amd import commit
@@ -338,6 +338,15 @@ def test_native_sharded_commit_c4_one_coset_per_rank(torch_mod):
     trace = commit.synthetic_trace(n_cols, log_n)
     ws = commit.witness_commit(trace, 1 << log_lde, cap)
     torch.cuda.synchronize()
+    # the one-GPU commit itself is pinned to the oracle's C4 cap (tools/make_bench_golden.py
+    # --chunk-cols 8), so every rank below is compared with oracle-checked slices
+    import json
+    import os
+    golden = json.load(open(os.path.join(os.path.dirname(__file__), "golden", "bench_caps.json")))["caps"]
+    want = [[int(x, 16) for x in row] for row in golden["C4/poseidon2"]["cap"]]
+    from boojum_amd.field import to_host
+    got = [[int(x) % ((1 << 64) - (1 << 32) + 1) for x in row] for row in to_host(ws.cap)]
+    assert got == want, "one-GPU C4 cap differs from the oracle's"
     hip = ctypes.CDLL("libamdhip64.so")
     hip.hipMemcpyAsync.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_size_t, ctypes.c_int, ctypes.c_void_p]
     mono = ws.scratch  # (C, n): the monomials in bj_lde_coeffs_d's bit-reversed format
