@@ -46,8 +46,15 @@ def main():
         e.record()
         torch.cuda.synchronize()
         ms = s.elapsed_time(e) / reps
+        # the same calls once more with the phase events on (bj_comm_set_timing)
+        comm.set_timing(True)
+        for _ in range(reps):
+            native_sharded_commit(comm, tr, n_cols, log_n, log_lde, cap, out=res)
+        torch.cuda.synchronize()
+        ph, calls = comm.phase_ms()
         out["%s_G%d" % (cfg, world)] = {
             "ms_per_rank": round(ms, 2), "ideal_elems_per_s": n_cols * n / (ms * 1e-3),
+            "phase_ms": {k: round(v / max(1, calls), 2) for k, v in ph.items()},
             "exchange": "none" if world == 1 else ("all-to-all (sender fold)" if world > (1 << log_lde)
                                                    else "all-gather"),
             "received_bytes_per_rank": 0 if world == 1 else (
