@@ -296,7 +296,7 @@ struct Run {
     uint32_t c0, c1;             // the chunk's global column range
 };
 
-// The column deal of sharded.py (_chunk_unit, _chunk_schedule, column_runs): chunk k is
+// The column deal (bj_sharded_columns; the CPU model of it is tests/sharded_model.py): chunk k is
 // G * c_k consecutive columns, c = u, u, 2u, 4u, ... capped at 32 rounded to u, u = 8/gcd(8, G);
 // rank P holds the P-th run of c_k.  One chunk (contiguous ownership) when C/G is not a
 // multiple of u, for a hasher without column continuation, or at G = 1 (nothing to overlap).
