@@ -52,7 +52,35 @@ def main():
             native_sharded_commit(comm, tr, n_cols, log_n, log_lde, cap, out=res)
         torch.cuda.synchronize()
         ph, calls = comm.phase_ms()
+        comm.set_timing(False)
+        recv = 0 if world == 1 else (
+            8 * n_cols * ((n << log_lde) // world) * (world - 1) // world if world > (1 << log_lde)
+            else 8 * n * n_cols * (world - 1) // world)
+        interfered = None
+        if recv and os.environ.get("PROBE_INTERFERE"):
+            # the same calls while a second, high-priority stream copies `recv` bytes device to
+            # device per call (what RCCL writes into this GPU's memory), to price the exchange's
+            # contention for CUs and HBM when it overlaps the compute
+            chunk = 256 << 20
+            a_buf = torch.empty(chunk // 8, dtype=torch.int64, device="cuda")
+            b_buf = torch.empty_like(a_buf)
+            side = torch.cuda.Stream(priority=-1)
+            s2, e2 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            torch.cuda.synchronize()
+            s2.record()
+            for _ in range(reps):
+                side.wait_stream(torch.cuda.current_stream())
+                with torch.cuda.stream(side):
+                    for _ in range(max(1, recv // chunk)):
+                        b_buf.copy_(a_buf)
+                native_sharded_commit(comm, tr, n_cols, log_n, log_lde, cap, out=res)
+                torch.cuda.current_stream().wait_stream(side)
+            e2.record()
+            torch.cuda.synchronize()
+            interfered = round(s2.elapsed_time(e2) / reps, 2)
+            del a_buf, b_buf
         out["%s_G%d" % (cfg, world)] = {
+            "ms_with_concurrent_copy_of_received_bytes": interfered,
             "ms_per_rank": round(ms, 2), "ideal_elems_per_s": n_cols * n / (ms * 1e-3),
             "phase_ms": {k: round(v / max(1, calls), 2) for k, v in ph.items()},
             "exchange": "none" if world == 1 else ("all-to-all (sender fold)" if world > (1 << log_lde)
