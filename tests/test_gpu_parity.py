@@ -195,6 +195,32 @@ def test_lde_batch(bj, c, log_n, log_d):
     eq(bj.field.to_host(bj.lde.transform_monomials_to_lde(m, 1 << log_d)), l_ref)
 
 
+@pytest.mark.parametrize("c,log_n,log_d", [(2, 10, 4), (1, 14, 4), (1, 13, 5), (1, 12, 5), (1, 15, 5)])
+def test_lde_high_degree(bj, c, log_n, log_d):
+    """LDE factors 16 and 32 (used_lde_degree = max(fri_lde_factor, quotient_degree),
+    prover.rs:313, is not bounded by 8), on both NTT paths."""
+    x = rand((c, 1 << log_n), 7 * log_d + log_n)
+    l = bj.lde.transform_raw_storages_to_lde(bj.field.to_device(x), 1 << log_d)
+    eq(bj.field.to_host(l), O.lde(x, log_d, threads=4)[1])
+
+
+@pytest.mark.slow
+@pytest.mark.parametrize("log_n", [24, 25])
+def test_transforms_past_the_ct_range(bj, log_n):
+    """Columns longer than 2^23 (outside the coset-folded CT passes) go through the DIF
+    network: forward with a coset, inverse, and an LDE x2, one column each."""
+    x = rand((1, 1 << log_n), 300 + log_n)
+    t = bj.field.to_device(x)
+    bj.fft.fft_natural_to_bitreversed(t, 7)
+    eq(bj.field.to_host(t)[0], O.fft_natural_to_bitreversed(x[0], 7))
+    t = bj.field.to_device(x)
+    bj.fft.ifft_natural_to_natural(t, 1)
+    eq(bj.field.to_host(t)[0], O.ifft_natural_to_natural(x[0], 1))
+    if log_n == 24:
+        l = bj.lde.transform_raw_storages_to_lde(bj.field.to_device(x), 2)
+        eq(bj.field.to_host(l), O.lde(x, 1, threads=8)[1])
+
+
 @pytest.mark.parametrize("log_n", [0, 1, 5, 12, 17, 18, 21])
 def test_lde_coeffs_exchange_format(bj, log_n):
     """bj_lde_coeffs_d: monomials c_j at bitrev_n(j), canonical (the multi-GPU exchange format)."""
