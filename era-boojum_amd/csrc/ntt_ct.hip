@@ -116,30 +116,33 @@ __device__ __forceinline__ uint32_t swz_gather(uint32_t e) { return e ^ ((e >> 9
 
 // Phase A' twiddles of stage v (register distance 16 >> v): pair q's group is lo(q) >> (5 - v),
 // the same for every thread.
+// gbase = 1 for a whole column; (2^u0 + g) for sub-column g of a column whose first u0 stages
+// are already done (the group index of global stage u0 + v is (g << v) + the local group).
 template <int V>
-__device__ __forceinline__ void tw_ct_headA(uint64_t* w, const uint64_t* __restrict__ ct) {
+__device__ __forceinline__ void tw_ct_headA(uint64_t* w, const uint64_t* __restrict__ ct, uint32_t gbase) {
     constexpr int HK = 16 >> V;
+    const uint64_t* base = ct + ((size_t)gbase << V);
 #pragma unroll
-    for (int q = 0; q < 16; q++) w[q] = ct[(1 << V) + (pair_lo(q, HK) >> (5 - V))];
+    for (int q = 0; q < 16; q++) w[q] = base[pair_lo(q, HK) >> (5 - V)];
 }
 
 // Phase B' twiddles of stage v >= 5 (rows 32 s + k, register distance 2^(R-1-v)):
 // group (32 s + lo(q)) >> (R - v).
 template <int R, int V>
-__device__ __forceinline__ void tw_ct_headB(uint64_t* w, const uint64_t* __restrict__ ct, uint32_t s) {
+__device__ __forceinline__ void tw_ct_headB(uint64_t* w, const uint64_t* __restrict__ ct, uint32_t s, uint32_t gbase) {
     constexpr int HK = 1 << (R - 1 - V);
-    const uint64_t* base = ct + (1u << V) + ((32u * s) >> (R - V));
+    const uint64_t* base = ct + ((size_t)gbase << V) + ((32u * s) >> (R - V));
 #pragma unroll
     for (int q = 0; q < 16; q++) w[q] = base[pair_lo(q, HK) >> (R - V)];
 }
 
 template <int R, int V>
-__device__ __forceinline__ void head_b_stage(uint64_t* x, const uint64_t* __restrict__ ct, uint32_t s) {
+__device__ __forceinline__ void head_b_stage(uint64_t* x, const uint64_t* __restrict__ ct, uint32_t s, uint32_t gbase) {
     if constexpr (V < R) {
         uint64_t w[16];
-        tw_ct_headB<R, V>(w, ct, s);
+        tw_ct_headB<R, V>(w, ct, s, gbase);
         ct_stage<(1 << (R - 1 - V))>(x, w);
-        head_b_stage<R, V + 1>(x, ct, s);
+        head_b_stage<R, V + 1>(x, ct, s, gbase);
     }
 }
 
@@ -165,12 +168,16 @@ __device__ __forceinline__ void head_unit(uint32_t bid, uint32_t n_cosets, bool 
 // carries it for the upper ones), i.e. scale the whole transform by kappa.
 // Grid: one dimension (head_unit): with the XCD-aware placement the source tile is fetched
 // from HBM once and re-read from L2 by the other cosets.
+// log_sub > 0: stages log_sub .. log_sub + R - 1 of columns of 2^(log_n + log_sub) words whose
+// first log_sub stages are done (launch_ct past 2^23): "column" c of the grid is sub-column
+// g = c mod 2^log_sub (2^log_n words at g 2^log_n) of column c >> log_sub, read at
+// src + column * src_stride + coset * src_coset_stride (in place on the coset outputs).
 template <int R, int MODE, bool KAPPA>
 __global__ __launch_bounds__(NT, 2) void ct_head_kernel(uint64_t* dst, size_t dst_col_stride, size_t coset_stride,
                                                         const uint64_t* src, size_t src_stride, uint32_t log_n,
                                                         const uint64_t* __restrict__ tab, size_t tab_stride,
                                                         uint64_t kappa, uint32_t n_cosets, uint32_t log_tiles,
-                                                        int xcd) {
+                                                        int xcd, uint32_t log_sub, size_t src_coset_stride) {
     constexpr int LOGW = 13 - R;
     constexpr uint32_t W = 1u << LOGW;
     constexpr uint32_t T = 1u << (R - 5);
@@ -180,9 +187,11 @@ __global__ __launch_bounds__(NT, 2) void ct_head_kernel(uint64_t* dst, size_t ds
     const size_t S = n >> R;
     uint32_t coset, unit;
     head_unit(blockIdx.x, n_cosets, xcd != 0, coset, unit);
-    const uint32_t col = unit >> log_tiles;
+    const uint32_t colv = unit >> log_tiles;
+    const uint32_t col = colv >> log_sub, sub = colv & ((1u << log_sub) - 1);
+    const uint32_t gbase = (1u << log_sub) + sub;
     const size_t o0 = (size_t)(unit & ((1u << log_tiles) - 1)) * W;
-    const uint64_t* sc = src + (size_t)col * src_stride;
+    const uint64_t* sc = src + (size_t)col * src_stride + (size_t)coset * src_coset_stride + ((size_t)sub << log_n);
     const uint64_t* ct = tab + (size_t)coset * tab_stride;
     const uint32_t w = tid & (W - 1);
     const uint32_t s = tid >> LOGW;
@@ -205,18 +214,18 @@ __global__ __launch_bounds__(NT, 2) void ct_head_kernel(uint64_t* dst, size_t ds
     // phase A': rows s + T k, stages 0..4
     {
         uint64_t wa[16], wb[16];
-        tw_ct_headA<0>(wa, ct);
-        tw_ct_headA<1>(wb, ct);
+        tw_ct_headA<0>(wa, ct, gbase);
+        tw_ct_headA<1>(wb, ct, gbase);
         if constexpr (KAPPA) {
 #pragma unroll
             for (int k = 0; k < 16; k += 4) mul4_by(x[k], x[k + 1], x[k + 2], x[k + 3], kappa);
         }
         ct_stage<16>(x, wa);
-        tw_ct_headA<2>(wa, ct);
+        tw_ct_headA<2>(wa, ct, gbase);
         ct_stage<8>(x, wb);
-        tw_ct_headA<3>(wb, ct);
+        tw_ct_headA<3>(wb, ct, gbase);
         ct_stage<4>(x, wa);
-        tw_ct_headA<4>(wa, ct);
+        tw_ct_headA<4>(wa, ct, gbase);
         ct_stage<2>(x, wb);
         ct_stage<1>(x, wa);
     }
@@ -231,8 +240,8 @@ __global__ __launch_bounds__(NT, 2) void ct_head_kernel(uint64_t* dst, size_t ds
     __syncthreads();
 #pragma unroll
     for (int k = 0; k < PT; k++) x[k] = lds[pd + k * W + ((k * W) >> 5)];
-    head_b_stage<R, 5>(x, ct, s);
-    uint64_t* dc = dst + (size_t)col * dst_col_stride + (size_t)coset * coset_stride;
+    head_b_stage<R, 5>(x, ct, s, gbase);
+    uint64_t* dc = dst + (size_t)col * dst_col_stride + (size_t)coset * coset_stride + ((size_t)sub << log_n);
 #pragma unroll
     for (int k = 0; k < PT; k++) dc[(size_t)(32 * s + k) * S + o] = x[k];
 }
@@ -468,7 +477,8 @@ void launch_head_R(int mode, bool kappa_on, dim3 g, uint64_t* dst, size_t dst_co
 #define BJ_CT_HEAD(M, K)                                                                                      \
     if constexpr (R >= 5)                                                                                     \
         hipLaunchKernelGGL((ct_head_kernel<R, M, K>), g1, dim3(NT), 0, st, dst, dst_col_stride, coset_stride, \
-                           src, src_stride, log_n, tab, tab_stride, kappa, g.z, log_tiles, xcd);             \
+                           src, src_stride, log_n, tab, tab_stride, kappa, g.z, log_tiles, xcd, 0u,       \
+                           (size_t)0);                                                                       \
     else                                                                                                      \
         hipLaunchKernelGGL((ct_head_small_kernel<R, M, K>), g1, dim3(NT), 0, st, dst, dst_col_stride,         \
                            coset_stride, src, src_stride, log_n, tab, tab_stride, kappa, g.z, log_tiles, xcd)
@@ -484,7 +494,10 @@ void launch_head_R(int mode, bool kappa_on, dim3 g, uint64_t* dst, size_t dst_co
 
 }  // namespace
 
-bool ct_ntt_supported(uint32_t log_n) { return log_n >= 13 && log_n <= 23; }
+// 2^13..2^23: head (log n - 13 stages) + tail (13).  2^24..2^26: a small head runs the first
+// log n - 23 stages over the whole column, the R = 10 head the next 10 on each 2^23-word
+// sub-column in place, then the tail.
+bool ct_ntt_supported(uint32_t log_n) { return log_n >= 13 && log_n <= 26; }
 
 hipError_t launch_ct_table(uint64_t* out, uint32_t log_n, bool inverse, uint64_t shift, uint64_t scale1,
                            hipStream_t st) {
@@ -523,7 +536,20 @@ hipError_t launch_ct(uint64_t* dst, size_t dst_col_stride, size_t coset_stride, 
     const dim3 g(n_cols, tiles, n_cosets);
     const int mode = src_bitrev ? 1 : 0;
     const bool k_on = kappa != 0;
-    switch (log_n - 13) {
+    if (log_n > 23) {
+        const uint32_t r1 = log_n - 23;
+        switch (r1) {
+            case 1: launch_head_R<1>(mode, k_on, g, dst, dst_col_stride, coset_stride, src, src_stride, log_n, tab, tab_stride, kappa, st); break;
+            case 2: launch_head_R<2>(mode, k_on, g, dst, dst_col_stride, coset_stride, src, src_stride, log_n, tab, tab_stride, kappa, st); break;
+            default: launch_head_R<3>(mode, k_on, g, dst, dst_col_stride, coset_stride, src, src_stride, log_n, tab, tab_stride, kappa, st); break;
+        }
+        // stages r1 .. r1 + 9 on the 2^r1 sub-columns of every column and coset, in place
+        const uint32_t sub_tiles_log = 23 - 13;
+        const size_t units = (size_t)n_cols * n_cosets << (r1 + sub_tiles_log);
+        hipLaunchKernelGGL((ct_head_kernel<10, 0, false>), dim3((unsigned)units), dim3(NT), 0, st, dst,
+                           dst_col_stride, coset_stride, dst, dst_col_stride, 23u, tab, tab_stride, (uint64_t)0,
+                           n_cosets, sub_tiles_log, 1, r1, coset_stride);
+    } else switch (log_n - 13) {
         case 0: launch_head_R<0>(mode, k_on, g, dst, dst_col_stride, coset_stride, src, src_stride, log_n, tab, tab_stride, kappa, st); break;
         case 1: launch_head_R<1>(mode, k_on, g, dst, dst_col_stride, coset_stride, src, src_stride, log_n, tab, tab_stride, kappa, st); break;
         case 2: launch_head_R<2>(mode, k_on, g, dst, dst_col_stride, coset_stride, src, src_stride, log_n, tab, tab_stride, kappa, st); break;

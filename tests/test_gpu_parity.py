@@ -205,10 +205,11 @@ def test_lde_high_degree(bj, c, log_n, log_d):
 
 
 @pytest.mark.slow
-@pytest.mark.parametrize("log_n", [24, 25])
-def test_transforms_past_the_ct_range(bj, log_n):
-    """Columns longer than 2^23 (outside the coset-folded CT passes) go through the DIF
-    network: forward with a coset, inverse, and an LDE x2, one column each."""
+@pytest.mark.parametrize("log_n", [24, 25, 26])
+def test_transforms_past_2_23(bj, log_n):
+    """Columns longer than 2^23: the CT passes run a small head over the whole column, the
+    R = 10 head on each 2^23-word sub-column, then the tail (launch_ct): forward with a coset,
+    inverse, and an LDE x2, one column each."""
     x = rand((1, 1 << log_n), 300 + log_n)
     t = bj.field.to_device(x)
     bj.fft.fft_natural_to_bitreversed(t, 7)

@@ -58,7 +58,7 @@ __global__ __launch_bounds__(NT, 2) void head_ablation(uint64_t* dst, size_t dst
     }
     auto twA = [&](uint64_t* wv, auto vtag) {
         constexpr int V = decltype(vtag)::value;
-        if constexpr (TWL) tw_ct_headA<V>(wv, ct);
+        if constexpr (TWL) tw_ct_headA<V>(wv, ct, 1u);
         else {
 #pragma unroll
             for (int q = 0; q < 16; q++) wv[q] = 0x123456789ull * (q + V + 1) + coset;
@@ -88,7 +88,7 @@ __global__ __launch_bounds__(NT, 2) void head_ablation(uint64_t* dst, size_t dst
         for (int k = 0; k < PT; k++) x[k] = lds[pd + k * W + ((k * W) >> 5)];
     }
     if constexpr (TWL) {
-        head_b_stage<R, 5>(x, ct, s);
+        head_b_stage<R, 5>(x, ct, s, 1u);
     } else {
         uint64_t wv[16];
 #pragma unroll
