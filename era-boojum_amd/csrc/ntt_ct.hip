@@ -168,11 +168,11 @@ __device__ __forceinline__ void head_unit(uint32_t bid, uint32_t n_cosets, bool 
 // carries it for the upper ones), i.e. scale the whole transform by kappa.
 // Grid: one dimension (head_unit): with the XCD-aware placement the source tile is fetched
 // from HBM once and re-read from L2 by the other cosets.
-// log_sub > 0: stages log_sub .. log_sub + R - 1 of columns of 2^(log_n + log_sub) words whose
+// SUB (log_sub > 0): stages log_sub .. log_sub + R - 1 of columns of 2^(log_n + log_sub) words whose
 // first log_sub stages are done (launch_ct past 2^23): "column" c of the grid is sub-column
 // g = c mod 2^log_sub (2^log_n words at g 2^log_n) of column c >> log_sub, read at
 // src + column * src_stride + coset * src_coset_stride (in place on the coset outputs).
-template <int R, int MODE, bool KAPPA>
+template <int R, int MODE, bool KAPPA, bool SUB = false>
 __global__ __launch_bounds__(NT, 2) void ct_head_kernel(uint64_t* dst, size_t dst_col_stride, size_t coset_stride,
                                                         const uint64_t* src, size_t src_stride, uint32_t log_n,
                                                         const uint64_t* __restrict__ tab, size_t tab_stride,
@@ -188,10 +188,10 @@ __global__ __launch_bounds__(NT, 2) void ct_head_kernel(uint64_t* dst, size_t ds
     uint32_t coset, unit;
     head_unit(blockIdx.x, n_cosets, xcd != 0, coset, unit);
     const uint32_t colv = unit >> log_tiles;
-    const uint32_t col = colv >> log_sub, sub = colv & ((1u << log_sub) - 1);
-    const uint32_t gbase = (1u << log_sub) + sub;
+    const uint32_t col = SUB ? colv >> log_sub : colv, sub = SUB ? colv & ((1u << log_sub) - 1) : 0;
+    const uint32_t gbase = SUB ? (1u << log_sub) + sub : 1;  // compile-time 1 for whole columns
     const size_t o0 = (size_t)(unit & ((1u << log_tiles) - 1)) * W;
-    const uint64_t* sc = src + (size_t)col * src_stride + (size_t)coset * src_coset_stride + ((size_t)sub << log_n);
+    const uint64_t* sc = src + (size_t)col * src_stride + (SUB ? (size_t)coset * src_coset_stride + ((size_t)sub << log_n) : 0);
     const uint64_t* ct = tab + (size_t)coset * tab_stride;
     const uint32_t w = tid & (W - 1);
     const uint32_t s = tid >> LOGW;
@@ -205,11 +205,29 @@ __global__ __launch_bounds__(NT, 2) void ct_head_kernel(uint64_t* dst, size_t ds
         const size_t run = (size_t)gl::bitrev32((uint32_t)(o0 + wg), log_n - R) << R;
 #pragma unroll
         for (int k = 0; k < PT; k++) x[k] = sc[run + sg + T * k];
+        if constexpr (R == 9) {
+            // bitrev_R(sg + T k) = bitrev_{R-5}(sg) * 32 + bitrev_5(k) (sg < T = 2^(R-5)); at R = 9
+            // the swizzle's bits 9..12 are bitrev_4(sg) and its XOR stays inside wg's 4 bits
+            // (W = 16), so the slot is a per-thread base plus bitrev_5(k) W, a compile-time offset
+            const uint32_t brs = gl::bitrev32(sg, R - 5);
+            const uint32_t base = (brs << 5) * W + (wg ^ (brs & 15));
 #pragma unroll
-        for (int k = 0; k < PT; k++) lds[swz_gather(gl::bitrev32(sg + T * k, R) * W + wg)] = x[k];
+            for (int k = 0; k < PT; k++) lds[base + gl::bitrev32((uint32_t)k, 5) * W] = x[k];
+        } else {
+#pragma unroll
+            for (int k = 0; k < PT; k++) lds[swz_gather(gl::bitrev32(sg + T * k, R) * W + wg)] = x[k];
+        }
         __syncthreads();
+        if constexpr (R >= 7 && R <= 9) {
+            // swz_gather((s + T k) W + w): bits 9..12 are (k >> 1) & 15 and the XOR stays inside w
+            // (R <= 9); at R = 5, 6 the compiler's own indexing is a little cheaper
+            const uint32_t sw = s * W;
 #pragma unroll
-        for (int k = 0; k < PT; k++) x[k] = lds[swz_gather((s + T * k) * W + w)];
+            for (int k = 0; k < PT; k++) x[k] = lds[sw + 256 * k + (w ^ ((k >> 1) & 15))];
+        } else {
+#pragma unroll
+            for (int k = 0; k < PT; k++) x[k] = lds[swz_gather((s + T * k) * W + w)];
+        }
     }
     // phase A': rows s + T k, stages 0..4
     {
@@ -241,7 +259,7 @@ __global__ __launch_bounds__(NT, 2) void ct_head_kernel(uint64_t* dst, size_t ds
 #pragma unroll
     for (int k = 0; k < PT; k++) x[k] = lds[pd + k * W + ((k * W) >> 5)];
     head_b_stage<R, 5>(x, ct, s, gbase);
-    uint64_t* dc = dst + (size_t)col * dst_col_stride + (size_t)coset * coset_stride + ((size_t)sub << log_n);
+    uint64_t* dc = dst + (size_t)col * dst_col_stride + (size_t)coset * coset_stride + (SUB ? ((size_t)sub << log_n) : 0);
 #pragma unroll
     for (int k = 0; k < PT; k++) dc[(size_t)(32 * s + k) * S + o] = x[k];
 }
@@ -546,7 +564,7 @@ hipError_t launch_ct(uint64_t* dst, size_t dst_col_stride, size_t coset_stride, 
         // stages r1 .. r1 + 9 on the 2^r1 sub-columns of every column and coset, in place
         const uint32_t sub_tiles_log = 23 - 13;
         const size_t units = (size_t)n_cols * n_cosets << (r1 + sub_tiles_log);
-        hipLaunchKernelGGL((ct_head_kernel<10, 0, false>), dim3((unsigned)units), dim3(NT), 0, st, dst,
+        hipLaunchKernelGGL((ct_head_kernel<10, 0, false, true>), dim3((unsigned)units), dim3(NT), 0, st, dst,
                            dst_col_stride, coset_stride, dst, dst_col_stride, 23u, tab, tab_stride, (uint64_t)0,
                            n_cosets, sub_tiles_log, 1, r1, coset_stride);
     } else switch (log_n - 13) {
