@@ -198,8 +198,11 @@ __global__ __launch_bounds__(NT, 2) void ct_head_kernel(uint64_t* dst, size_t ds
     const size_t o = o0 + w;
     uint64_t x[PT];
     if constexpr (MODE == 0) {
+        // row s + T k of the tile: a wave-uniform row base (scalar) plus a per-thread 32-bit
+        // index, so each load is one instruction with no address VALU
+        const uint32_t vi = (uint32_t)(s * S + o);
 #pragma unroll
-        for (int k = 0; k < PT; k++) x[k] = sc[(size_t)(s + T * k) * S + o];
+        for (int k = 0; k < PT; k++) x[k] = (sc + (size_t)T * k * S)[vi];
     } else {
         const uint32_t wg = tid / T, sg = tid % T;
         const size_t run = (size_t)gl::bitrev32((uint32_t)(o0 + wg), log_n - R) << R;
@@ -260,8 +263,9 @@ __global__ __launch_bounds__(NT, 2) void ct_head_kernel(uint64_t* dst, size_t ds
     for (int k = 0; k < PT; k++) x[k] = lds[pd + k * W + ((k * W) >> 5)];
     head_b_stage<R, 5>(x, ct, s, gbase);
     uint64_t* dc = dst + (size_t)col * dst_col_stride + (size_t)coset * coset_stride + (SUB ? ((size_t)sub << log_n) : 0);
+    const uint32_t vo = (uint32_t)(32 * s * S + o);
 #pragma unroll
-    for (int k = 0; k < PT; k++) dc[(size_t)(32 * s + k) * S + o] = x[k];
+    for (int k = 0; k < PT; k++) (dc + (size_t)k * S)[vo] = x[k];
 }
 
 // --------------------------------------------------------- small heads (R <= 4)

@@ -8,6 +8,7 @@
 //   3 no LDS               gather staging and the A'->B' exchange removed (loads kept)
 //   4 no twiddle loads     twiddles from registers
 //   5 butterflies only     1 + 2 + 3 + 4
+//   6 the production kernel as it now stands (variant 0 is the sequence this tool copied)
 // Build: hipcc -O3 -std=c++17 --offload-arch=gfx950 -I era-boojum_amd/csrc -o tools/ntt_head_ablation tools/ntt_head_ablation.hip
 #include "../era-boojum_amd/csrc/ntt_ct.hip"
 #include <cstdio>
@@ -142,7 +143,25 @@ int main() {
     hipEvent_t a, b;
     CHECK(hipEventCreate(&a));
     CHECK(hipEventCreate(&b));
-    for (int v = 0; v < 6; v++) {
+    for (int v = 0; v < 7; v++) {
+        if (v == 6) {  // the production kernel (csrc/ntt_ct.hip as built into this tool)
+            const int xcd = 1;
+            hipLaunchKernelGGL((bj::ct_head_kernel<9, 1, false>), g, dim3(bj::NT), 0, 0, dst, n * cosets, n,
+                               (const uint64_t*)src, n, log_n, (const uint64_t*)tab, n, (uint64_t)0, cosets,
+                               log_tiles, xcd, 0u, (size_t)0);
+            CHECK(hipDeviceSynchronize());
+            CHECK(hipEventRecord(a));
+            for (int r = 0; r < 3; r++)
+                hipLaunchKernelGGL((bj::ct_head_kernel<9, 1, false>), g, dim3(bj::NT), 0, 0, dst, n * cosets, n,
+                                   (const uint64_t*)src, n, log_n, (const uint64_t*)tab, n, (uint64_t)0, cosets,
+                                   log_tiles, xcd, 0u, (size_t)0);
+            CHECK(hipEventRecord(b));
+            CHECK(hipEventSynchronize(b));
+            float ms = 0;
+            CHECK(hipEventElapsedTime(&ms, a, b));
+            printf("{\"variant\": 6, \"name\": \"production kernel\", \"ms\": %.3f}\n", ms / 3);
+            continue;
+        }
         hipLaunchKernelGGL(ks[v], g, dim3(bj::NT), 0, 0, dst, n * cosets, n, src, n, log_n, tab, n, cosets, log_tiles);
         CHECK(hipGetLastError());
         CHECK(hipDeviceSynchronize());

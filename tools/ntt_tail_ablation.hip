@@ -10,6 +10,8 @@
 //   5 butterflies only     1 + 2 + 3 + 4
 //   6 nontemporal stores   the full kernel with streaming stores
 //   7 ... and loads        streaming loads and stores
+//   8 uniform-base loads/stores ((d + 256 k)[t] instead of d[t + 256 k])
+//   9 the full kernel again (box drift between the first and the last timing)
 // Build: hipcc -O3 -std=c++17 --offload-arch=gfx950 -I era-boojum_amd/csrc -o tools/ntt_tail_ablation tools/ntt_tail_ablation.hip
 #include "../era-boojum_amd/csrc/ntt_ct.hip"
 #include <cstdio>
@@ -21,12 +23,13 @@ template <int ABL>
 __device__ __forceinline__ void tail_unit_body(uint64_t* lds, uint64_t* d, const uint64_t* __restrict__ ct, size_t q,
                                                uint32_t u0) {
     constexpr bool LOAD = ABL != 1 && ABL != 5, STORE = ABL != 2 && ABL != 5, EXCH = ABL != 3 && ABL != 5,
-                   TWL = ABL != 4 && ABL != 5, NTS = ABL == 6 || ABL == 7, NTL = ABL == 7;
+                   TWL = ABL != 4 && ABL != 5, NTS = ABL == 6 || ABL == 7, NTL = ABL == 7, SADDR = ABL == 8;
     const uint32_t t = threadIdx.x;
     uint64_t x[PT], wa[16], wb[16];
     if constexpr (LOAD) {
 #pragma unroll
-        for (int k = 0; k < PT; k++) x[k] = NTL ? __builtin_nontemporal_load(d + t + NT * k) : d[t + NT * k];
+        for (int k = 0; k < PT; k++)
+            x[k] = NTL ? __builtin_nontemporal_load(d + t + NT * k) : (SADDR ? (d + NT * k)[t] : d[t + NT * k]);
     } else {
 #pragma unroll
         for (int k = 0; k < PT; k++) x[k] = (uint64_t)(t + 1) * (2 * k + 1) + q;
@@ -111,6 +114,7 @@ __device__ __forceinline__ void tail_unit_body(uint64_t* lds, uint64_t* d, const
 #pragma unroll
         for (int k = 0; k < PT; k++) {
             if constexpr (NTS) __builtin_nontemporal_store(canon_u64(x[k]), d + t + NT * k);
+            else if constexpr (SADDR) (d + NT * k)[t] = canon_u64(x[k]);
             else d[t + NT * k] = canon_u64(x[k]);
         }
     } else {
@@ -171,9 +175,10 @@ int main() {
     using K = void (*)(uint64_t*, size_t, size_t, uint32_t, const uint64_t*, size_t);
     const K ks[] = {bj::tail_ablation<0>, bj::tail_ablation<1>, bj::tail_ablation<2>,
                     bj::tail_ablation<3>, bj::tail_ablation<4>, bj::tail_ablation<5>,
-                    bj::tail_ablation<6>, bj::tail_ablation<7>};
+                    bj::tail_ablation<6>, bj::tail_ablation<7>, bj::tail_ablation<8>, bj::tail_ablation<0>};
     const char* names[] = {"full", "no global load", "no store", "no LDS exchanges", "no twiddle loads",
-                           "butterflies only", "nontemporal stores", "nontemporal loads and stores"};
+                           "butterflies only", "nontemporal stores", "nontemporal loads and stores",
+                           "uniform-base addressing", "full (again)"};
     hipEvent_t a, b;
     CHECK(hipEventCreate(&a));
     CHECK(hipEventCreate(&b));
@@ -195,7 +200,7 @@ int main() {
         CHECK(hipEventElapsedTime(&ms, a, b));
         printf("{\"variant\": \"persistent %d blocks/CU\", \"ms\": %.3f}\n", mult, ms / 3);
     }
-    for (int v = 0; v < 8; v++) {
+    for (int v = 0; v < 10; v++) {
         hipLaunchKernelGGL(ks[v], g, dim3(bj::NT), 0, 0, buf, n * cosets, n, log_n, tab, n);
         CHECK(hipGetLastError());
         CHECK(hipDeviceSynchronize());
