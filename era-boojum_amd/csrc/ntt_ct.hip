@@ -168,9 +168,9 @@ __device__ __forceinline__ void head_unit(uint32_t bid, uint32_t n_cosets, bool 
 // carries it for the upper ones), i.e. scale the whole transform by kappa.
 // Grid: one dimension (head_unit): with the XCD-aware placement the source tile is fetched
 // from HBM once and re-read from L2 by the other cosets.
-// SUB (log_sub > 0): stages log_sub .. log_sub + R - 1 of columns of 2^(log_n + log_sub) words whose
-// first log_sub stages are done (launch_ct past 2^23): "column" c of the grid is sub-column
-// g = c mod 2^log_sub (2^log_n words at g 2^log_n) of column c >> log_sub, read at
+// SUB (log_sub > 0): stages log_sub .. log_sub + R - 1 of columns of 2^(log_n + log_sub) words
+// whose first log_sub stages are done (launch_ct past 2^23): "column" c of the grid is
+// sub-column g = c mod 2^log_sub (2^log_n words at g 2^log_n) of column c >> log_sub, read at
 // src + column * src_stride + coset * src_coset_stride (in place on the coset outputs).
 template <int R, int MODE, bool KAPPA, bool SUB = false>
 __global__ __launch_bounds__(NT, 2) void ct_head_kernel(uint64_t* dst, size_t dst_col_stride, size_t coset_stride,
@@ -191,7 +191,8 @@ __global__ __launch_bounds__(NT, 2) void ct_head_kernel(uint64_t* dst, size_t ds
     const uint32_t col = SUB ? colv >> log_sub : colv, sub = SUB ? colv & ((1u << log_sub) - 1) : 0;
     const uint32_t gbase = SUB ? (1u << log_sub) + sub : 1;  // compile-time 1 for whole columns
     const size_t o0 = (size_t)(unit & ((1u << log_tiles) - 1)) * W;
-    const uint64_t* sc = src + (size_t)col * src_stride + (SUB ? (size_t)coset * src_coset_stride + ((size_t)sub << log_n) : 0);
+    const uint64_t* sc =
+        src + (size_t)col * src_stride + (SUB ? (size_t)coset * src_coset_stride + ((size_t)sub << log_n) : 0);
     const uint64_t* ct = tab + (size_t)coset * tab_stride;
     const uint32_t w = tid & (W - 1);
     const uint32_t s = tid >> LOGW;
@@ -262,7 +263,8 @@ __global__ __launch_bounds__(NT, 2) void ct_head_kernel(uint64_t* dst, size_t ds
 #pragma unroll
     for (int k = 0; k < PT; k++) x[k] = lds[pd + k * W + ((k * W) >> 5)];
     head_b_stage<R, 5>(x, ct, s, gbase);
-    uint64_t* dc = dst + (size_t)col * dst_col_stride + (size_t)coset * coset_stride + (SUB ? ((size_t)sub << log_n) : 0);
+    uint64_t* dc =
+        dst + (size_t)col * dst_col_stride + (size_t)coset * coset_stride + (SUB ? ((size_t)sub << log_n) : 0);
     const uint32_t vo = (uint32_t)(32 * s * S + o);
 #pragma unroll
     for (int k = 0; k < PT; k++) (dc + (size_t)k * S)[vo] = x[k];
