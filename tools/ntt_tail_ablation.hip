@@ -12,6 +12,7 @@
 //   7 ... and loads        streaming loads and stores
 //   8 uniform-base loads/stores ((d + 256 k)[t] instead of d[t + 256 k])
 //   9 the full kernel again (box drift between the first and the last timing)
+//  10 no final C -> A exchange: each thread stores its 32 contiguous elements as 16-byte writes
 // Build: hipcc -O3 -std=c++17 --offload-arch=gfx950 -I era-boojum_amd/csrc -o tools/ntt_tail_ablation tools/ntt_tail_ablation.hip
 #include "../era-boojum_amd/csrc/ntt_ct.hip"
 #include <cstdio>
@@ -23,7 +24,8 @@ template <int ABL>
 __device__ __forceinline__ void tail_unit_body(uint64_t* lds, uint64_t* d, const uint64_t* __restrict__ ct, size_t q,
                                                uint32_t u0) {
     constexpr bool LOAD = ABL != 1 && ABL != 5, STORE = ABL != 2 && ABL != 5, EXCH = ABL != 3 && ABL != 5,
-                   TWL = ABL != 4 && ABL != 5, NTS = ABL == 6 || ABL == 7, NTL = ABL == 7, SADDR = ABL == 8;
+                   TWL = ABL != 4 && ABL != 5, NTS = ABL == 6 || ABL == 7, NTL = ABL == 7, SADDR = ABL == 8,
+                   CSTORE = ABL == 10;
     const uint32_t t = threadIdx.x;
     uint64_t x[PT], wa[16], wb[16];
     if constexpr (LOAD) {
@@ -102,6 +104,18 @@ __device__ __forceinline__ void tail_unit_body(uint64_t* lds, uint64_t* d, const
     twC(wa, std::integral_constant<int, 12>{});
     ct_stage<2>(x, wb);
     ct_stage<1>(x, wa);
+    if constexpr (CSTORE) {
+        // no final exchange: layout C (element 32 t + k) stored as it stands, 16 bytes per lane
+        uint64_t* dt = d + 32 * t;
+#pragma unroll
+        for (int k = 0; k < PT; k += 2) {
+            ulonglong2 v;
+            v.x = canon_u64(x[k]);
+            v.y = canon_u64(x[k + 1]);
+            *reinterpret_cast<ulonglong2*>(dt + k) = v;
+        }
+        return;
+    }
     if constexpr (EXCH) {
         __syncthreads();
 #pragma unroll
@@ -175,10 +189,12 @@ int main() {
     using K = void (*)(uint64_t*, size_t, size_t, uint32_t, const uint64_t*, size_t);
     const K ks[] = {bj::tail_ablation<0>, bj::tail_ablation<1>, bj::tail_ablation<2>,
                     bj::tail_ablation<3>, bj::tail_ablation<4>, bj::tail_ablation<5>,
-                    bj::tail_ablation<6>, bj::tail_ablation<7>, bj::tail_ablation<8>, bj::tail_ablation<0>};
+                    bj::tail_ablation<6>, bj::tail_ablation<7>, bj::tail_ablation<8>, bj::tail_ablation<0>,
+                    bj::tail_ablation<10>, bj::tail_ablation<0>};
     const char* names[] = {"full", "no global load", "no store", "no LDS exchanges", "no twiddle loads",
                            "butterflies only", "nontemporal stores", "nontemporal loads and stores",
-                           "uniform-base addressing", "full (again)"};
+                           "uniform-base addressing", "full (again)", "no final exchange: 16-byte stores from layout C",
+                           "full (third)"};
     hipEvent_t a, b;
     CHECK(hipEventCreate(&a));
     CHECK(hipEventCreate(&b));
@@ -200,7 +216,7 @@ int main() {
         CHECK(hipEventElapsedTime(&ms, a, b));
         printf("{\"variant\": \"persistent %d blocks/CU\", \"ms\": %.3f}\n", mult, ms / 3);
     }
-    for (int v = 0; v < 10; v++) {
+    for (int v = 0; v < 12; v++) {
         hipLaunchKernelGGL(ks[v], g, dim3(bj::NT), 0, 0, buf, n * cosets, n, log_n, tab, n);
         CHECK(hipGetLastError());
         CHECK(hipDeviceSynchronize());
