@@ -70,6 +70,7 @@ SIGNATURES = {
     "bj_comm_init_local": ([_vp, _int, ctypes.POINTER(_vp)], _int),
     "bj_comm_init_callback": ([_int, _int, EXCHANGE_FN, _vp, _int, ctypes.POINTER(_vp)], _int),
     "bj_comm_destroy": ([_vp], _int),
+    "bj_comm_exchange_d": ([_vp, _int, _vp, _vp, _sz, _vp], _int),
     "bj_comm_set_timing": ([_vp, _int], _int),
     "bj_comm_phase_ms": ([_vp, ctypes.POINTER(ctypes.c_float), ctypes.POINTER(_int)], _int),
     "bj_sharded_columns": ([_u32, _u32, _u32, _int, ctypes.POINTER(_u32)], _int),

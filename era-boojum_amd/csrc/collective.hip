@@ -250,8 +250,12 @@ int callback_exchange(bj_comm* c, int kind, const void* send, void* recv, size_t
 }
 
 // recv (world x bytes) <- concat over ranks of send (bytes); send may be recv + rank * bytes
+// A one-rank RCCL communicator still runs the RCCL call (a copy inside RCCL), so the calls the
+// multi-GPU run depends on are exercised on a one-GPU box (tests/test_gpu_rccl.py).
+bool is_rccl(const bj_comm* c) { return c->kind == bj_comm::RCCL_OWNED || c->kind == bj_comm::RCCL_WRAPPED; }
+
 int all_gather(bj_comm* c, const void* send, void* recv, size_t bytes, hipStream_t st) {
-    if (c->world == 1) {
+    if (c->world == 1 && !is_rccl(c)) {
         if (send != recv && bytes) HIP_CHECK(hipMemcpyAsync(recv, send, bytes, hipMemcpyDeviceToDevice, st), "memcpy");
         return BJ_OK;
     }
@@ -264,7 +268,7 @@ int all_gather(bj_comm* c, const void* send, void* recv, size_t bytes, hipStream
 
 // recv block p (bytes) <- block `rank` of rank p's send (world x bytes)
 int all_to_all(bj_comm* c, const void* send, void* recv, size_t bytes, hipStream_t st) {
-    if (c->world == 1) {
+    if (c->world == 1 && !is_rccl(c)) {
         if (send != recv && bytes) HIP_CHECK(hipMemcpyAsync(recv, send, bytes, hipMemcpyDeviceToDevice, st), "memcpy");
         return BJ_OK;
     }
@@ -525,6 +529,15 @@ int bj_comm_phase_ms(bj_comm* c, float* ms_out4, int* calls_out) {
     if (calls_out) *calls_out = c->timed_calls;
     c->timed_calls = 0;
     return rc;
+}
+
+int bj_comm_exchange_d(bj_comm* c, int kind, const void* send, void* recv, size_t bytes, void* stream) {
+    if (!c) return err(BJ_EINVAL, "null communicator");
+    if (kind != BJ_XCHG_ALL_GATHER && kind != BJ_XCHG_ALL_TO_ALL) return err(BJ_EINVAL, "unknown exchange kind");
+    if (bytes % 8) return err(BJ_EINVAL, "bytes must be a multiple of 8");
+    if (bytes && (!send || !recv)) return err(BJ_EINVAL, "null buffer");
+    hipStream_t st = reinterpret_cast<hipStream_t>(stream);
+    return kind == BJ_XCHG_ALL_GATHER ? all_gather(c, send, recv, bytes, st) : all_to_all(c, send, recv, bytes, st);
 }
 
 int bj_comm_destroy(bj_comm* c) {

@@ -307,6 +307,11 @@ int bj_comm_local_group_destroy(void* group);
 int bj_comm_init_local(void* group, int rank, bj_comm** out);
 int bj_comm_init_callback(int world, int rank, bj_exchange_fn exchange, void* user, int host_staged, bj_comm** out);
 int bj_comm_destroy(bj_comm* comm);
+/* One data exchange of bj_sharded_commit_d's kinds (BJ_XCHG_ALL_GATHER / BJ_XCHG_ALL_TO_ALL, the
+ * layouts above) over `comm`, ordered on `stream`: the transport alone, so a caller can check its
+ * communicator before a commit.  Collective; bytes per rank block, a multiple of 8.  An RCCL
+ * communicator issues the RCCL call even at world 1 (ncclAllGather; grouped ncclSend/ncclRecv). */
+int bj_comm_exchange_d(bj_comm* comm, int kind, const void* send, void* recv, size_t bytes, void* stream);
 /* Phase timing of bj_sharded_commit_d on this communicator (no reference counterpart: the
  * reference logs its phase times, merkle_tree.rs:162-167, prover.rs:345).  on != 0: every later
  * call records HIP events on its compute stream around the inverse transforms (+ folds), the

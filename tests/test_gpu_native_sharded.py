@@ -382,3 +382,51 @@ def test_native_sharded_commit_c4_one_coset_per_rank(torch_mod):
         torch.cuda.empty_cache()
     del ws, trace, mono
     torch.cuda.empty_cache()
+
+
+def test_local_exchange_layouts():
+    """bj_comm_exchange_d's two layouts over the in-process group at G = 4 (the same calls the
+    commit issues per chunk): all-gather recv block p = rank p's send; all-to-all recv block p =
+    block `rank` of rank p's send."""
+    import torch
+    from boojum_amd._lib import call
+    from boojum_amd.field import stream_of
+    from boojum_amd.sharded import XCHG_ALL_GATHER, XCHG_ALL_TO_ALL, LocalGroup
+    world, m = 4, 1000
+    group = LocalGroup(world)
+    got, errors = [None] * world, []
+
+    def rank_main(P):
+        try:
+            torch.cuda.set_device(0)
+            s = torch.cuda.Stream()
+            with torch.cuda.stream(s):
+                comm = group.comm(P)
+                ag_send = torch.arange(m, dtype=torch.int64, device="cuda") + 10**6 * P
+                ag_recv = torch.empty(world * m, dtype=torch.int64, device="cuda")
+                # all-to-all send block q (destined to rank q) = 10^6 P + 10^3 q + i
+                a2a_send = (torch.arange(world * m, dtype=torch.int64, device="cuda") % m
+                            + 10**6 * P + 10**3 * (torch.arange(world * m, device="cuda") // m))
+                a2a_recv = torch.empty(world * m, dtype=torch.int64, device="cuda")
+                for kind, snd, rcv in ((XCHG_ALL_GATHER, ag_send, ag_recv), (XCHG_ALL_TO_ALL, a2a_send, a2a_recv)):
+                    call("bj_comm_exchange_d", comm.handle, kind, snd.data_ptr(), rcv.data_ptr(), 8 * m, stream_of(rcv))
+                s.synchronize()
+                got[P] = (ag_recv.cpu(), a2a_recv.cpu())
+                comm.close()
+        except Exception as e:  # noqa: BLE001 - reported below
+            errors.append((P, repr(e)))
+
+    threads = [threading.Thread(target=rank_main, args=(P,), daemon=True) for P in range(world)]
+    for t in threads:
+        t.start()
+    for t in threads:
+        t.join(timeout=60)
+    assert not any(t.is_alive() for t in threads), "a rank did not finish"
+    group.close()
+    assert not errors, errors
+    i = torch.arange(m, dtype=torch.int64)
+    for P in range(world):
+        ag, a2a = got[P]
+        for p in range(world):
+            assert torch.equal(ag[p * m:(p + 1) * m], i + 10**6 * p)
+            assert torch.equal(a2a[p * m:(p + 1) * m], i + 10**6 * p + 10**3 * P)

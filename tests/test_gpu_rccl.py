@@ -42,3 +42,49 @@ def test_native_commit_over_process_group_comm(pg, log_lde, log_k):
         assert torch.equal(r.leaves, ws.leaves) and torch.equal(r.nodes, ws.nodes) and torch.equal(r.cap, ws.cap)
     finally:
         comm.close()
+
+
+def _exchange(comm, kind, send, recv, nbytes):
+    from boojum_amd._lib import call
+    from boojum_amd.field import stream_of
+    call("bj_comm_exchange_d", comm.handle, kind, send.data_ptr(), recv.data_ptr(), nbytes, stream_of(recv))
+
+
+@pytest.mark.parametrize("make", ["world1", "process_group"])
+def test_rccl_exchange_calls(pg, make):
+    """bj_comm_exchange_d over a one-rank RCCL communicator issues the real RCCL calls the N > 1
+    commit makes (ncclAllGather, in place and not; grouped ncclSend / ncclRecv for the
+    all-to-all), which the commit itself skips at world 1: the bytes must arrive unchanged."""
+    torch = pg
+    from boojum_amd.sharded import XCHG_ALL_GATHER, XCHG_ALL_TO_ALL, NativeComm
+    comm = NativeComm.rccl_world1() if make == "world1" else NativeComm.rccl()
+    try:
+        g = torch.Generator(device="cuda").manual_seed(7)
+        for n in (1, 1000, 1 << 20):
+            src = torch.randint(-2**62, 2**62, (n,), dtype=torch.int64, device="cuda", generator=g)
+            for kind in (XCHG_ALL_GATHER, XCHG_ALL_TO_ALL):
+                dst = torch.zeros_like(src)
+                _exchange(comm, kind, src, dst, 8 * n)
+                torch.cuda.synchronize()
+                assert torch.equal(dst, src)
+            inplace = src.clone()
+            _exchange(comm, XCHG_ALL_GATHER, inplace, inplace, 8 * n)
+            torch.cuda.synchronize()
+            assert torch.equal(inplace, src)
+    finally:
+        comm.close()
+
+
+def test_exchange_rejects_bad_arguments(pg):
+    torch = pg
+    from boojum_amd._lib import BoojumError
+    from boojum_amd.sharded import NativeComm
+    comm = NativeComm.rccl_world1()
+    try:
+        a = torch.zeros(4, dtype=torch.int64, device="cuda")
+        with pytest.raises(BoojumError):
+            _exchange(comm, 7, a, a, 32)
+        with pytest.raises(BoojumError):
+            _exchange(comm, 0, a, a, 12)
+    finally:
+        comm.close()
