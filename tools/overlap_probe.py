@@ -35,6 +35,9 @@ def main():
     state = torch.empty((nl, 4), dtype=torch.int64, device="cuda")
     sa = torch.cuda.current_stream()
     sb = torch.cuda.Stream()
+    # the LDE on a high-priority stream: the dispatcher then places NTT blocks first when a CU
+    # frees room (BJ_LEAF_LDS_BYTES caps the leaf blocks per CU so that room exists)
+    hp = torch.cuda.Stream(priority=-1)
 
     def seq():
         st = sa.cuda_stream
@@ -42,16 +45,19 @@ def main():
         call("bj_merkle_leaves_d", ws.lde.data_ptr(), n_cols, nl, nl, ws.leaves.data_ptr(), st)
         call("bj_merkle_nodes_d", ws.leaves.data_ptr(), nl, cap, ws.nodes.data_ptr(), st)
 
-    def chunked(cc, two_streams):
+    def chunked(cc, two_streams, lde_stream=None):
         k_total = n_cols // cc
         leaf_stream = sb if two_streams else sa
+        la = lde_stream or sa
+        if lde_stream is not None:
+            la.wait_stream(sa)
         evs = []
         for k in range(k_total):
             c0 = k * cc
             call("bj_lde_d", trace[c0].data_ptr(), cc, n, log_n, log_lde, ws.scratch[c0].data_ptr(),
-                 ws.lde[c0].data_ptr(), sa.cuda_stream)
+                 ws.lde[c0].data_ptr(), la.cuda_stream)
             e = torch.cuda.Event()
-            e.record(sa)
+            e.record(la)
             evs.append(e)
         for k in range(k_total):
             c0 = k * cc
@@ -63,6 +69,8 @@ def main():
         call("bj_merkle_nodes_d", ws.leaves.data_ptr(), nl, cap, ws.nodes.data_ptr(), leaf_stream.cuda_stream)
         if two_streams:
             sa.wait_stream(sb)
+        if lde_stream is not None:
+            sa.wait_stream(la)
 
     def timeit(fn, reps=3):
         fn()
@@ -81,6 +89,9 @@ def main():
         assert torch.equal(ws.cap, ref_cap), "chunked cap differs"
         out["overlap%d_ms" % cc] = timeit(lambda: chunked(cc, True))
         assert torch.equal(ws.cap, ref_cap), "overlap cap differs"
+        out["overlap%d_hp_ms" % cc] = timeit(lambda: chunked(cc, True, hp))
+        assert torch.equal(ws.cap, ref_cap), "overlap (high-priority LDE) cap differs"
+    out["leaf_lds_bytes"] = int(os.environ.get("BJ_LEAF_LDS_BYTES", "0"))
     print(json.dumps(out))
 
 

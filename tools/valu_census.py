@@ -107,9 +107,9 @@ def straight_line(instrs):
 def ntt_census():
     """Per-wave VALU instructions and issue slots of the coset-folded CT passes (ntt_ct.hip):
     ct_head_kernel<R, MODE, KAPPA> for R = log n - 13 (forward: MODE 1, no kappa; inverse:
-    MODE 0 with kappa) and ct_tail_kernel. They are fully unrolled (no loops), so one wave
+    MODE 0 with kappa) and ct_tail_kernel<true>. They are fully unrolled (no loops), so one wave
     executes each instruction once; bench.py multiplies by the launched waves for the NTT
-    phase's VALU utilisation. (The tail's uniform canon_out branch is counted taken.)"""
+    phase's VALU utilisation."""
     dis = disassemble("ntt_ct")
     out = {}
     for r in range(5, 11):
@@ -118,7 +118,9 @@ def ntt_census():
             if ins:
                 v, s = straight_line(ins)
                 out.setdefault(key, {})[str(r)] = {"valu": v, "slots": s}
-    v, s = straight_line(parse(kernel_lines(dis, "ct_tail_kernel")))
+    # the LDE's tails canonicalise their output (ct_tail_kernel<true>); match that one
+    # instantiation only (the name prefix alone also matches ct_tail_kernel<false>)
+    v, s = straight_line(parse(kernel_lines(dis, "ct_tail_kernelILb1E")))
     out["tail"] = {"valu": v, "slots": s}
     out["waves_per_block"] = 4
     out["elements_per_block"] = 8192
