@@ -181,7 +181,8 @@ def test_host_seams_concurrent_threads(bj):
 
 @pytest.mark.parametrize("c,log_n,log_d", [(1, 0, 1), (2, 1, 1), (3, 3, 2), (5, 6, 3), (4, 12, 1), (3, 13, 2),
                                            (3, 14, 3), (5, 15, 1), (1, 16, 2), (7, 13, 3),
-                                           (2, 16, 3), (1, 17, 1), (2, 18, 2), (1, 19, 3), (1, 20, 1)])
+                                           (2, 16, 3), (1, 17, 1), (2, 18, 2), (1, 19, 3), (1, 20, 1),
+                                           (2, 22, 2)])
 def test_lde_batch(bj, c, log_n, log_d):
     x = rand((c, 1 << log_n), c * 100 + log_n)
     t = bj.field.to_device(x)
@@ -236,7 +237,7 @@ def test_lde_coeffs_exchange_format(bj, log_n):
     eq(bj.field.to_host(out), want)
 
 
-@pytest.mark.parametrize("log_n,log_d", [(18, 1), (18, 3), (23, 1)])
+@pytest.mark.parametrize("log_n,log_d", [(18, 1), (18, 3), (22, 2), (23, 1)])
 def test_lde_edge_columns_large(bj, log_n, log_d):
     """Zero / p-1 / impulse / non-canonical columns on the register-resident NTT sizes."""
     n = 1 << log_n
