@@ -76,6 +76,8 @@ hipError_t launch_fold_all(uint64_t* dst, size_t dst_col_stride, size_t dst_shar
 namespace bj {
 // ntt_ct.hip: coset-folded Cooley-Tukey passes for 2^13 <= n <= 2^23
 bool ct_ntt_supported(uint32_t log_n);
+// entries of one CT table (the coset-folded table + the power-of-two phases' prescale tables)
+size_t ct_table_len(uint32_t log_n);
 hipError_t launch_ct_table(uint64_t* out, uint32_t log_n, bool inverse, uint64_t shift, uint64_t scale1,
                            hipStream_t st);
 hipError_t launch_ct(uint64_t* dst, size_t dst_col_stride, size_t coset_stride, uint32_t n_cosets,

@@ -170,7 +170,7 @@ int get_ct(uint32_t log_n, bool inverse, uint64_t shift_, const uint64_t** out) 
     auto it = c.ct.find(key);
     if (it != c.ct.end()) { *out = it->second; return BJ_OK; }
     uint64_t* p = nullptr;
-    HIP_TRY(hipMalloc(&p, ((size_t)1 << log_n) * sizeof(uint64_t)), "hipMalloc(ct table)");
+    HIP_TRY(hipMalloc(&p, bj::ct_table_len(log_n) * sizeof(uint64_t)), "hipMalloc(ct table)");
     hipStream_t st;
     HIP_TRY(hipStreamCreateWithFlags(&st, hipStreamNonBlocking), "hipStreamCreate");
     const uint64_t scale1 = inverse ? gl::canon(gl::inv((uint64_t)1 << log_n)) : 1;
@@ -183,7 +183,7 @@ int get_ct(uint32_t log_n, bool inverse, uint64_t shift_, const uint64_t** out) 
     return BJ_OK;
 }
 
-// The D coset tables of an LDE, table i (shift 7 * w_{nD}^bitrev(i)) at out + i * n.
+// The D coset tables of an LDE, table i (shift 7 * w_{nD}^bitrev(i)) at out + i * ct_table_len.
 int get_ct_lde(uint32_t log_n, uint32_t log_d, const uint64_t** out) {
     int dev = 0;
     HIP_TRY(hipGetDevice(&dev), "hipGetDevice");
@@ -192,7 +192,7 @@ int get_ct_lde(uint32_t log_n, uint32_t log_d, const uint64_t** out) {
     auto key = std::make_tuple(dev, log_n, log_d);
     auto it = c.ct_lde.find(key);
     if (it != c.ct_lde.end()) { *out = it->second; return BJ_OK; }
-    const size_t n = (size_t)1 << log_n;
+    const size_t n = bj::ct_table_len(log_n);
     const uint32_t D = 1u << log_d;
     uint64_t* p = nullptr;
     HIP_TRY(hipMalloc(&p, D * n * sizeof(uint64_t)), "hipMalloc(ct lde tables)");
@@ -293,8 +293,9 @@ int lde_forward(uint64_t* lde, size_t col_stride, size_t coset_stride, uint32_t 
     if (bj::ct_ntt_supported(log_n)) {
         const uint64_t* tabs;
         if (int r = get_ct_lde(log_n, log_lde, &tabs)) return r;
+        const size_t L = bj::ct_table_len(log_n);
         HIP_TRY(bj::launch_ct(lde, col_stride, coset_stride, n_cosets, src, src_stride, src_bitrev, n_cols, log_n,
-                              tabs + (size_t)first * n, n, 0, true, st),
+                              tabs + (size_t)first * L, L, 0, true, st),
                 "coset fft");
         return BJ_OK;
     }

@@ -29,6 +29,7 @@
 #include <hip/hip_runtime.h>
 #include "gl.hpp"
 #include "gl_asm.hpp"
+#include "ntt_pow2.hpp"
 #include "bj_internal.hpp"
 
 namespace bj {
@@ -95,6 +96,59 @@ __device__ __forceinline__ uint64_t canon_u64(uint64_t v) {
     split2(v, a0, a1);
     glasm::canon_x1(a0, a1, z0, z1);
     return join2(z0, z1);
+}
+
+// ------------------------------------------------- power-of-two register phases (round 2)
+//
+// A register phase of r <= 5 stages acts on 2^r elements of one group of the network, whose
+// polynomial Q is evaluated on a coset sigma <w>: with the elements at coefficient distance M,
+// the phase is a 2^r-point DFT of (q_k sigma^(M k)) with the root w_{2^r}. So
+// each phase multiplies its inputs by a prescale table once (one general product per element)
+// and runs a DFT whose twiddles are +-2^e (csrc/ntt_pow2.hpp): 5 stages cost ~15% fewer
+// instructions than the coset-folded general stages (tools/pow2_bench.hip).
+//
+// Table extension (after the n-entry CT table of a shift s, ct_table_len):
+//   [0, 32)              HA[k] = s^((n/32) k)                       head phase A' (rows s + T k)
+//   [32, 32 + 2^R)       HB[r] = sigma5_(r >> (R-5))^((n >> R) (r & (2^(R-5) - 1)))   phase B'
+//   [EXT_TA, +32 2^u0)   TA[q][k] = sigma_u0(q)^(256 k) (x n^-1 for the inverse, 18 <= log n <= 23)
+//   [ext_tb, +32 2^(u0+5)) TB[g][k] = sigma_(u0+5)(g)^(8 k)
+// with sigma_u(g) = s w_n^bitrev_u(g), the coset of group g after u stages.
+constexpr size_t EXT_HB = 32;
+constexpr size_t EXT_TA = 32 + 1024;
+__host__ __device__ __forceinline__ size_t ext_tb(uint32_t u0) { return EXT_TA + ((size_t)32 << u0); }
+
+template <int LOG, bool INV, int B>
+__device__ __forceinline__ void dft_p2(uint64_t* x) {
+    using namespace p2dft;
+    if constexpr (LOG == 1) { if constexpr (INV) dft2_inv<B>(x); else dft2_fwd<B>(x); }
+    if constexpr (LOG == 2) { if constexpr (INV) dft4_inv<B>(x); else dft4_fwd<B>(x); }
+    if constexpr (LOG == 3) { if constexpr (INV) dft8_inv<B>(x); else dft8_fwd<B>(x); }
+    if constexpr (LOG == 4) { if constexpr (INV) dft16_inv<B>(x); else dft16_fwd<B>(x); }
+    if constexpr (LOG == 5) { if constexpr (INV) dft32_inv<B>(x); else dft32_fwd<B>(x); }
+}
+
+// the 32 / 2^LOG register groups of a phase, each a 2^LOG-point DFT
+template <int LOG, bool INV, int G = 0>
+__device__ __forceinline__ void dft_p2_groups(uint64_t* x) {
+    if constexpr (G < (32 >> LOG)) {
+        dft_p2<LOG, INV, (G << LOG)>(x);
+        dft_p2_groups<LOG, INV, G + 1>(x);
+    }
+}
+
+// x[k] *= f[k] for k < 32 (general products; outputs any u64 representative)
+__device__ __forceinline__ void prescale32(uint64_t* x, const uint64_t* f) {
+#pragma unroll
+    for (int k = 0; k < PT; k += 4) {
+        uint32_t z0[4], z1[4];
+        glasm::mul_x4((uint32_t)x[k], (uint32_t)(x[k] >> 32), (uint32_t)f[k], (uint32_t)(f[k] >> 32), z0[0], z1[0],
+                      (uint32_t)x[k + 1], (uint32_t)(x[k + 1] >> 32), (uint32_t)f[k + 1], (uint32_t)(f[k + 1] >> 32),
+                      z0[1], z1[1], (uint32_t)x[k + 2], (uint32_t)(x[k + 2] >> 32), (uint32_t)f[k + 2],
+                      (uint32_t)(f[k + 2] >> 32), z0[2], z1[2], (uint32_t)x[k + 3], (uint32_t)(x[k + 3] >> 32),
+                      (uint32_t)f[k + 3], (uint32_t)(f[k + 3] >> 32), z0[3], z1[3]);
+#pragma unroll
+        for (int i = 0; i < 4; i++) x[k + i] = join2(z0[i], z1[i]);
+    }
 }
 
 // ------------------------------------------------------------------- head
@@ -172,7 +226,9 @@ __device__ __forceinline__ void head_unit(uint32_t bid, uint32_t n_cosets, bool 
 // whose first log_sub stages are done (launch_ct past 2^23): "column" c of the grid is
 // sub-column g = c mod 2^log_sub (2^log_n words at g 2^log_n) of column c >> log_sub, read at
 // src + column * src_stride + coset * src_coset_stride (in place on the coset outputs).
-template <int R, int MODE, bool KAPPA, bool SUB = false>
+// P2 (whole columns, 5 <= R <= 10, no KAPPA): the power-of-two form of both phases, with the
+// prescale tables after the CT table (INV: the inverse root; n^-1 then sits in the tail's TA).
+template <int R, int MODE, bool KAPPA, bool SUB = false, bool P2 = false, bool INV = false>
 __global__ __launch_bounds__(NT, 2) void ct_head_kernel(uint64_t* dst, size_t dst_col_stride, size_t coset_stride,
                                                         const uint64_t* src, size_t src_stride, uint32_t log_n,
                                                         const uint64_t* __restrict__ tab, size_t tab_stride,
@@ -233,8 +289,13 @@ __global__ __launch_bounds__(NT, 2) void ct_head_kernel(uint64_t* dst, size_t ds
             for (int k = 0; k < PT; k++) x[k] = lds[swz_gather((s + T * k) * W + w)];
         }
     }
+    static_assert(!P2 || (!KAPPA && !SUB), "the power-of-two head takes whole columns, n^-1 in the tail");
     // phase A': rows s + T k, stages 0..4
-    {
+    if constexpr (P2) {
+        // coefficient distance n/32 between the rows: prescale s^((n/32) k), wave-uniform
+        prescale32(x, ct + n);
+        dft_p2<5, INV, 0>(x);
+    } else {
         uint64_t wa[16], wb[16];
         tw_ct_headA<0>(wa, ct, gbase);
         tw_ct_headA<1>(wb, ct, gbase);
@@ -262,7 +323,15 @@ __global__ __launch_bounds__(NT, 2) void ct_head_kernel(uint64_t* dst, size_t ds
     __syncthreads();
 #pragma unroll
     for (int k = 0; k < PT; k++) x[k] = lds[pd + k * W + ((k * W) >> 5)];
-    head_b_stage<R, 5>(x, ct, s, gbase);
+    if constexpr (P2) {
+        // rows 32 s + k: groups of 2^(R-5) rows after phase A', coefficient distance n >> R
+        if constexpr (R > 5) {
+            prescale32(x, ct + n + EXT_HB + 32 * s);
+            dft_p2_groups<R - 5, INV>(x);
+        }
+    } else {
+        head_b_stage<R, 5>(x, ct, s, gbase);
+    }
     uint64_t* dc =
         dst + (size_t)col * dst_col_stride + (size_t)coset * coset_stride + (SUB ? ((size_t)sub << log_n) : 0);
     const uint32_t vo = (uint32_t)(32 * s * S + o);
@@ -276,7 +345,7 @@ __global__ __launch_bounds__(NT, 2) void ct_head_kernel(uint64_t* dst, size_t ds
 // x 2^(13-R) columns as above, and each thread holds all 2^R rows of C = 2^(5-R) columns
 // (columns t + 256 i), so every butterfly is thread-local and needs no LDS; the group index
 // of stage v is the row's top v bits, a compile-time register property, so every twiddle is
-// a wave-uniform (scalar) load. R = 0 (n = 2^13) is the load / gather / kappa step alone.
+// a wave-uniform (scalar) load. R = 0 (n = 2^13) is the load / gather step alone.
 // x[r * C + i] holds row r of column i; the pairs of stage v are (r, r + 2^(R-1-v)), i.e.
 // registers k and k + 2^(R-1-v) C.
 template <int R, int V>
@@ -328,17 +397,12 @@ __global__ __launch_bounds__(NT, 2) void ct_head_small_kernel(uint64_t* dst, siz
             for (int r = 0; r < (1 << R); r++) x[r * C + i] = sc[run + gl::bitrev32(r, R)];
         }
     }
-    if constexpr (KAPPA) {
-        if constexpr (R == 0) {
-            // stage 0 is the tail's: its lower operands are the first half of the column
+    // R = 0 has no stage of its own: an inverse's n^-1 then sits in the tail's TA table
+    // (kappa_in_tail), and launch_ct never passes kappa here
+    if constexpr (KAPPA && R > 0) {
+        // stage-0 lower operands: rows below 2^(R-1), registers 0..15
 #pragma unroll
-            for (int i = 0; i < C; i++)
-                if (o0 + t + NT * i < (S >> 1)) x[i] = gl::mul(x[i], kappa);
-        } else {
-            // stage-0 lower operands: rows below 2^(R-1), registers 0..15
-#pragma unroll
-            for (int k = 0; k < 16; k += 4) mul4_by(x[k], x[k + 1], x[k + 2], x[k + 3], kappa);
-        }
+        for (int k = 0; k < 16; k += 4) mul4_by(x[k], x[k + 1], x[k + 2], x[k + 3], kappa);
     }
     small_stage<R, 0>(x, ct);
     uint64_t* dc = dst + (size_t)col * dst_col_stride + (size_t)coset * coset_stride;
@@ -367,26 +431,6 @@ __device__ __forceinline__ uint32_t tail_base_c(uint32_t t) { return 33 * t; }
 __device__ __forceinline__ constexpr uint32_t tail_off_a(int k) { return 264 * k; }
 __device__ __forceinline__ constexpr uint32_t tail_off_b(int k) { return 8 * k + (k >> 2); }
 
-// phase A (element t + 256 k, local stage v = 0..4): group (q << v) + (lo(q) >> (5 - v)),
-// wave-uniform.
-template <int V>
-__device__ __forceinline__ void tw_ct_tailA(uint64_t* w, const uint64_t* __restrict__ ct, uint32_t u0, size_t q) {
-    constexpr int HK = 16 >> V;
-    const uint64_t* base = ct + ((size_t)1 << (u0 + V)) + (q << V);
-#pragma unroll
-    for (int p = 0; p < 16; p++) w[p] = base[pair_lo(p, HK) >> (5 - V)];
-}
-
-// phase B (element (thi << 8) | (k << 3) | tlo, v = 5..9): (q << v) + (thi << (v-5)) + (lo >> (10-v)).
-template <int V>
-__device__ __forceinline__ void tw_ct_tailB(uint64_t* w, const uint64_t* __restrict__ ct, uint32_t u0, size_t q,
-                                            uint32_t thi) {
-    constexpr int HK = 16 >> (V - 5);
-    const uint64_t* base = ct + ((size_t)1 << (u0 + V)) + (q << V) + ((size_t)thi << (V - 5));
-#pragma unroll
-    for (int p = 0; p < 16; p++) w[p] = base[pair_lo(p, HK) >> (10 - V)];
-}
-
 // phase C (element 32 t + k, v = 10..12): (q << v) + (t << (v-8)) + (lo >> (13-v)).
 template <int V>
 __device__ __forceinline__ void tw_ct_tailC(uint64_t* w, const uint64_t* __restrict__ ct, uint32_t u0, size_t q,
@@ -398,8 +442,12 @@ __device__ __forceinline__ void tw_ct_tailC(uint64_t* w, const uint64_t* __restr
 }
 
 // CANON: canonicalise the output (a template parameter: a run-time branch per element made the
-// compiler wait on each epilogue LDS read separately).
-template <bool CANON>
+// compiler wait on each epilogue LDS read separately). INV: the inverse root (the table is an
+// inverse table). Phases A and B (local stages 0..4 and 5..9) run in the power-of-two form:
+// block q's polynomial is evaluated on sigma_u0(q) <w_8192>, so phase A prescales element
+// t + 256 k by TA[q][k] = sigma_u0(q)^(256 k) and phase B element (thi, 8 k + tlo) by
+// TB[(q << 5) | thi][k]; phase C (3 stages) keeps the coset-folded general twiddles.
+template <bool CANON, bool INV>
 __global__ __launch_bounds__(NT, 2) void ct_tail_kernel(uint64_t* dst, size_t dst_col_stride, size_t coset_stride,
                                                         uint32_t log_n, const uint64_t* __restrict__ tab,
                                                         size_t tab_stride) {
@@ -409,37 +457,22 @@ __global__ __launch_bounds__(NT, 2) void ct_tail_kernel(uint64_t* dst, size_t ds
     const uint32_t u0 = log_n - 13;
     uint64_t* d = dst + (size_t)blockIdx.x * dst_col_stride + (size_t)blockIdx.z * coset_stride + q * TILE;
     const uint64_t* ct = tab + (size_t)blockIdx.z * tab_stride;
+    const uint64_t* ext = ct + ((size_t)1 << log_n);
     uint64_t x[PT], wa[16], wb[16];
 #pragma unroll
     for (int k = 0; k < PT; k++) x[k] = d[t + NT * k];
-    tw_ct_tailA<0>(wa, ct, u0, q);
-    tw_ct_tailA<1>(wb, ct, u0, q);
-    ct_stage<16>(x, wa);
-    tw_ct_tailA<2>(wa, ct, u0, q);
-    ct_stage<8>(x, wb);
-    tw_ct_tailA<3>(wb, ct, u0, q);
-    ct_stage<4>(x, wa);
-    tw_ct_tailA<4>(wa, ct, u0, q);
-    ct_stage<2>(x, wb);
+    prescale32(x, ext + EXT_TA + q * 32);
+    dft_p2<5, INV, 0>(x);
     const uint32_t tlo = t & 7, thi = t >> 3;
     const uint32_t ba = tail_base_a(t), bb = tail_base_b(thi, tlo), bc = tail_base_c(t);
-    tw_ct_tailB<5>(wb, ct, u0, q, thi);
-    ct_stage<1>(x, wa);
 #pragma unroll
     for (int k = 0; k < PT; k++) lds[ba + tail_off_a(k)] = x[k];
     __syncthreads();
 #pragma unroll
     for (int k = 0; k < PT; k++) x[k] = lds[bb + tail_off_b(k)];
-    tw_ct_tailB<6>(wa, ct, u0, q, thi);
-    ct_stage<16>(x, wb);
-    tw_ct_tailB<7>(wb, ct, u0, q, thi);
-    ct_stage<8>(x, wa);
-    tw_ct_tailB<8>(wa, ct, u0, q, thi);
-    ct_stage<4>(x, wb);
-    tw_ct_tailB<9>(wb, ct, u0, q, thi);
-    ct_stage<2>(x, wa);
+    prescale32(x, ext + ext_tb(u0) + (((q << 5) | thi) << 5));
+    dft_p2<5, INV, 0>(x);
     tw_ct_tailC<10>(wa, ct, u0, q, t);
-    ct_stage<1>(x, wb);
     __syncthreads();
 #pragma unroll
     for (int k = 0; k < PT; k++) lds[bb + tail_off_b(k)] = x[k];
@@ -485,11 +518,50 @@ __global__ void ct_table_kernel(uint64_t* out, uint32_t log_n, uint64_t w_n, Shi
     }
 }
 
+// The prescale tables after the CT table (layout at EXT_HB / EXT_TA / ext_tb above). w_n is the
+// transform's root (inverted for the inverse), s its shift; ta_scale multiplies TA (n^-1 for the
+// inverse transforms whose head runs in the power-of-two form, 1 otherwise).
+__global__ void ct_ext_kernel(uint64_t* ext, uint32_t log_n, uint64_t w_n, uint64_t s, uint64_t ta_scale, size_t len) {
+    const size_t n = (size_t)1 << log_n;
+    const uint32_t u0 = log_n - 13, R = u0;
+    for (size_t i = blockIdx.x * (size_t)blockDim.x + threadIdx.x; i < len; i += (size_t)gridDim.x * blockDim.x) {
+        uint64_t v;
+        if (i < EXT_HB) {
+            v = gl::pow(s, (n >> 5) * i);
+        } else if (i < EXT_TA) {
+            const size_t j = i - EXT_HB;
+            if (R >= 5 && j < ((size_t)1 << R)) {
+                const uint32_t g = (uint32_t)(j >> (R - 5));
+                const uint64_t m = j & (((size_t)1 << (R - 5)) - 1);
+                const uint64_t sigma = gl::mul(s, gl::pow(w_n, gl::bitrev32(g, 5)));
+                v = gl::pow(sigma, (n >> R) * m);
+            } else {
+                v = 0;
+            }
+        } else if (i < ext_tb(u0)) {
+            const size_t j = i - EXT_TA;
+            const uint64_t sigma = gl::mul(s, gl::pow(w_n, gl::bitrev32((uint32_t)(j >> 5), u0)));
+            v = gl::mul(gl::pow(sigma, 256 * (j & 31)), ta_scale);
+        } else {
+            const size_t j = i - ext_tb(u0);
+            const uint64_t sigma = gl::mul(s, gl::pow(w_n, gl::bitrev32((uint32_t)(j >> 5), u0 + 5)));
+            v = gl::pow(sigma, 8 * (j & 31));
+        }
+        ext[i] = gl::canon(v);
+    }
+}
+
 __global__ __launch_bounds__(256) void scale_kernel(uint64_t* cols, size_t stride, size_t n, uint64_t k) {
     uint64_t* c = cols + (size_t)blockIdx.y * stride;
     for (size_t i = blockIdx.x * (size_t)blockDim.x + threadIdx.x; i < n; i += (size_t)gridDim.x * blockDim.x)
         c[i] = gl::canon(gl::mul(c[i], k));
 }
+
+// the heads of 2^18 .. 2^23 run in the power-of-two form (n^-1 of an inverse then in the tail)
+constexpr bool p2_head(uint32_t log_n) { return log_n >= 18 && log_n <= 23; }
+// where an inverse's n^-1 sits in the tail's TA table: the power-of-two heads, and 2^13, whose
+// head (R = 0) has no stage of its own (the general heads scale their own stage 0)
+constexpr bool kappa_in_tail(uint32_t log_n) { return p2_head(log_n) || log_n == 13; }
 
 template <int R>
 void launch_head_R(int mode, bool kappa_on, dim3 g, uint64_t* dst, size_t dst_col_stride, size_t coset_stride,
@@ -498,6 +570,24 @@ void launch_head_R(int mode, bool kappa_on, dim3 g, uint64_t* dst, size_t dst_co
     const uint32_t log_tiles = log_n - 13;
     const dim3 g1(g.x * g.y * g.z);
     const int xcd = ((g.x * g.y) % 8) == 0 ? 1 : 0;  // units (column x tile) in whole runs of 8
+    if constexpr (R >= 5) {
+        if (p2_head(log_n)) {
+            // the inverse (kappa != 0) folds n^-1 into its tail's TA table
+#define BJ_CT_HEAD_P2(M, I)                                                                                    \
+    hipLaunchKernelGGL((ct_head_kernel<R, M, false, false, true, I>), g1, dim3(NT), 0, st, dst, dst_col_stride, \
+                       coset_stride, src, src_stride, log_n, tab, tab_stride, (uint64_t)0, g.z, log_tiles, xcd, \
+                       0u, (size_t)0)
+            if (mode == 0) {
+                if (kappa_on) BJ_CT_HEAD_P2(0, true);
+                else BJ_CT_HEAD_P2(0, false);
+            } else {
+                if (kappa_on) BJ_CT_HEAD_P2(1, true);
+                else BJ_CT_HEAD_P2(1, false);
+            }
+#undef BJ_CT_HEAD_P2
+            return;
+        }
+    }
 #define BJ_CT_HEAD(M, K)                                                                                      \
     if constexpr (R >= 5)                                                                                     \
         hipLaunchKernelGGL((ct_head_kernel<R, M, K>), g1, dim3(NT), 0, st, dst, dst_col_stride, coset_stride, \
@@ -523,6 +613,13 @@ void launch_head_R(int mode, bool kappa_on, dim3 g, uint64_t* dst, size_t dst_co
 // sub-column in place, then the tail.
 bool ct_ntt_supported(uint32_t log_n) { return log_n >= 13 && log_n <= 26; }
 
+size_t ct_table_len(uint32_t log_n) {
+    const size_t n = (size_t)1 << log_n;
+    if (!ct_ntt_supported(log_n)) return n;
+    const uint32_t u0 = log_n - 13;
+    return n + ext_tb(u0) + ((size_t)32 << (u0 + 5));
+}
+
 hipError_t launch_ct_table(uint64_t* out, uint32_t log_n, bool inverse, uint64_t shift, uint64_t scale1,
                            hipStream_t st) {
     uint64_t w = gl::domain_generator(log_n);
@@ -534,6 +631,14 @@ hipError_t launch_ct_table(uint64_t* out, uint32_t log_n, bool inverse, uint64_t
     if (blocks > 8192) blocks = 8192;
     hipLaunchKernelGGL(ct_table_kernel, dim3((unsigned)blocks), dim3(256), 0, st, out, log_n, w, spw,
                        gl::canon(scale1));
+    if (ct_ntt_supported(log_n)) {
+        const size_t len = ct_table_len(log_n) - n;
+        const uint64_t ta_scale = inverse && kappa_in_tail(log_n) ? gl::canon(scale1) : 1;
+        size_t eb = (len + 255) / 256;
+        if (eb > 8192) eb = 8192;
+        hipLaunchKernelGGL(ct_ext_kernel, dim3((unsigned)eb), dim3(256), 0, st, out + n, log_n, w, gl::canon(shift),
+                           ta_scale, len);
+    }
     return hipGetLastError();
 }
 
@@ -548,8 +653,10 @@ hipError_t launch_scale(uint64_t* cols, size_t stride, uint32_t n_cols, size_t n
 // Coset-folded CT transform(s), natural -> bit-reversed, for n_cosets twiddle tables at
 // tab + i * tab_stride. Output (c, i, r) at dst + c * dst_col_stride + i * coset_stride + r.
 // src_bitrev: source holds c_j at bitrev_n(j) (never in place); otherwise natural (in place
-// allowed when dst == src and n_cosets == 1). kappa != 0: scale by kappa (the table's CT[1]
-// must already carry it).
+// allowed when dst == src and n_cosets == 1). kappa != 0 marks an inverse transform scaled by
+// kappa: the tables must be inverse tables made with scale1 = kappa (launch_ct_table), which
+// carry it (CT[1] for the general heads, TA for the power-of-two ones). Tables are
+// ct_table_len(log_n) entries each.
 hipError_t launch_ct(uint64_t* dst, size_t dst_col_stride, size_t coset_stride, uint32_t n_cosets,
                      const uint64_t* src, size_t src_stride, bool src_bitrev, uint32_t n_cols, uint32_t log_n,
                      const uint64_t* tab, size_t tab_stride, uint64_t kappa, bool canon_out, hipStream_t st) {
@@ -574,7 +681,7 @@ hipError_t launch_ct(uint64_t* dst, size_t dst_col_stride, size_t coset_stride, 
                            dst_col_stride, coset_stride, dst, dst_col_stride, 23u, tab, tab_stride, (uint64_t)0,
                            n_cosets, sub_tiles_log, 1, r1, coset_stride);
     } else switch (log_n - 13) {
-        case 0: launch_head_R<0>(mode, k_on, g, dst, dst_col_stride, coset_stride, src, src_stride, log_n, tab, tab_stride, kappa, st); break;
+        case 0: launch_head_R<0>(mode, false, g, dst, dst_col_stride, coset_stride, src, src_stride, log_n, tab, tab_stride, kappa, st); break;
         case 1: launch_head_R<1>(mode, k_on, g, dst, dst_col_stride, coset_stride, src, src_stride, log_n, tab, tab_stride, kappa, st); break;
         case 2: launch_head_R<2>(mode, k_on, g, dst, dst_col_stride, coset_stride, src, src_stride, log_n, tab, tab_stride, kappa, st); break;
         case 3: launch_head_R<3>(mode, k_on, g, dst, dst_col_stride, coset_stride, src, src_stride, log_n, tab, tab_stride, kappa, st); break;
@@ -586,12 +693,16 @@ hipError_t launch_ct(uint64_t* dst, size_t dst_col_stride, size_t coset_stride, 
         case 9: launch_head_R<9>(mode, k_on, g, dst, dst_col_stride, coset_stride, src, src_stride, log_n, tab, tab_stride, kappa, st); break;
         default: launch_head_R<10>(mode, k_on, g, dst, dst_col_stride, coset_stride, src, src_stride, log_n, tab, tab_stride, kappa, st); break;
     }
-    if (canon_out)
-        hipLaunchKernelGGL(ct_tail_kernel<true>, g, dim3(NT), 0, st, dst, dst_col_stride, coset_stride, log_n, tab,
-                           tab_stride);
-    else
-        hipLaunchKernelGGL(ct_tail_kernel<false>, g, dim3(NT), 0, st, dst, dst_col_stride, coset_stride, log_n, tab,
-                           tab_stride);
+#define BJ_CT_TAIL(C, I) \
+    hipLaunchKernelGGL((ct_tail_kernel<C, I>), g, dim3(NT), 0, st, dst, dst_col_stride, coset_stride, log_n, tab, tab_stride)
+    if (canon_out) {
+        if (k_on) BJ_CT_TAIL(true, true);
+        else BJ_CT_TAIL(true, false);
+    } else {
+        if (k_on) BJ_CT_TAIL(false, true);
+        else BJ_CT_TAIL(false, false);
+    }
+#undef BJ_CT_TAIL
     return hipGetLastError();
 }
 

@@ -2,7 +2,7 @@
 # rocprofv3 evidence for the C3 bench: the default bench line (with the CPU baseline), a
 # kernel-trace stats run, one PMC pass per counter group, the FETCH_SIZE / WRITE_SIZE
 # calibration on known byte counts (tools/fetch_calibration.hip), the per-rank compute probe,
-# and (when built) the butterfly and tail-ablation microbenchmarks.
+# and (when built) the butterfly and power-of-two DFT microbenchmarks.
 # usage: bash scripts/profile.sh TAG
 set -u
 TAG=${1:-r2}
@@ -26,9 +26,9 @@ timeout -s KILL 60 rocprofv3 --pmc WRITE_SIZE --output-format csv -d $OUT/cal_wr
 echo calibration ok
 timeout -k 10 300 python3 tools/shard_compute_probe.py > $OUT/shard_compute.log 2>&1 || { echo "probe rc=$?"; tail -5 $OUT/shard_compute.log; exit 1; }
 tail -1 $OUT/shard_compute.log
-if [ -x tools/ntt_tail_ablation ] && [ -x tools/bfly_bench ]; then
+if [ -x tools/pow2_bench ] && [ -x tools/bfly_bench ]; then
   timeout -k 10 120 ./tools/bfly_bench > $OUT/bfly_bench.log 2>&1 || { echo "bfly rc=$?"; exit 1; }
-  timeout -k 10 120 ./tools/ntt_tail_ablation > $OUT/ntt_tail_ablation.log 2>&1 || { echo "ablation rc=$?"; exit 1; }
+  timeout -k 10 120 ./tools/pow2_bench > $OUT/pow2_bench.log 2>&1 || { echo "pow2 rc=$?"; exit 1; }
   echo microbench ok
 fi
 echo done

@@ -129,9 +129,10 @@ int main() {
     uint64_t *src = nullptr, *dst = nullptr, *tab = nullptr;
     CHECK(hipMalloc(&src, n * cols * 8));
     CHECK(hipMalloc(&dst, n * cols * cosets * 8));
-    CHECK(hipMalloc(&tab, n * cosets * 8));
+    const size_t L = bj::ct_table_len(log_n);  // the CT table + the power-of-two prescale tables
+    CHECK(hipMalloc(&tab, L * cosets * 8));
     CHECK(hipMemset(src, 1, n * cols * 8));
-    for (uint32_t c = 0; c < cosets; c++) CHECK(bj::launch_ct_table(tab + c * n, log_n, false, 7 + c, 1, 0));
+    for (uint32_t c = 0; c < cosets; c++) CHECK(bj::launch_ct_table(tab + c * L, log_n, false, 7 + c, 1, 0));
     CHECK(hipDeviceSynchronize());
     const uint32_t log_tiles = log_n - 13;
     const dim3 g(cols * (1u << log_tiles) * cosets);
@@ -147,13 +148,13 @@ int main() {
         if (v == 6) {  // the production kernel (csrc/ntt_ct.hip as built into this tool)
             const int xcd = 1;
             hipLaunchKernelGGL((bj::ct_head_kernel<9, 1, false>), g, dim3(bj::NT), 0, 0, dst, n * cosets, n,
-                               (const uint64_t*)src, n, log_n, (const uint64_t*)tab, n, (uint64_t)0, cosets,
+                               (const uint64_t*)src, n, log_n, (const uint64_t*)tab, L, (uint64_t)0, cosets,
                                log_tiles, xcd, 0u, (size_t)0);
             CHECK(hipDeviceSynchronize());
             CHECK(hipEventRecord(a));
             for (int r = 0; r < 3; r++)
                 hipLaunchKernelGGL((bj::ct_head_kernel<9, 1, false>), g, dim3(bj::NT), 0, 0, dst, n * cosets, n,
-                                   (const uint64_t*)src, n, log_n, (const uint64_t*)tab, n, (uint64_t)0, cosets,
+                                   (const uint64_t*)src, n, log_n, (const uint64_t*)tab, L, (uint64_t)0, cosets,
                                    log_tiles, xcd, 0u, (size_t)0);
             CHECK(hipEventRecord(b));
             CHECK(hipEventSynchronize(b));
@@ -162,12 +163,12 @@ int main() {
             printf("{\"variant\": 6, \"name\": \"production kernel\", \"ms\": %.3f}\n", ms / 3);
             continue;
         }
-        hipLaunchKernelGGL(ks[v], g, dim3(bj::NT), 0, 0, dst, n * cosets, n, src, n, log_n, tab, n, cosets, log_tiles);
+        hipLaunchKernelGGL(ks[v], g, dim3(bj::NT), 0, 0, dst, n * cosets, n, src, n, log_n, tab, L, cosets, log_tiles);
         CHECK(hipGetLastError());
         CHECK(hipDeviceSynchronize());
         CHECK(hipEventRecord(a));
         for (int r = 0; r < 3; r++)
-            hipLaunchKernelGGL(ks[v], g, dim3(bj::NT), 0, 0, dst, n * cosets, n, src, n, log_n, tab, n, cosets,
+            hipLaunchKernelGGL(ks[v], g, dim3(bj::NT), 0, 0, dst, n * cosets, n, src, n, log_n, tab, L, cosets,
                                log_tiles);
         CHECK(hipEventRecord(b));
         CHECK(hipEventSynchronize(b));

@@ -107,21 +107,25 @@ def straight_line(instrs):
 def ntt_census():
     """Per-wave VALU instructions and issue slots of the coset-folded CT passes (ntt_ct.hip):
     ct_head_kernel<R, MODE, KAPPA> for R = log n - 13 (forward: MODE 1, no kappa; inverse:
-    MODE 0 with kappa) and ct_tail_kernel<true>. They are fully unrolled (no loops), so one wave
+    MODE 0, inverse roots) and ct_tail_kernel<true, INV>. They are fully unrolled (no loops), so one wave
     executes each instruction once; bench.py multiplies by the launched waves for the NTT
     phase's VALU utilisation."""
     dis = disassemble("ntt_ct")
     out = {}
     for r in range(5, 11):
-        for key, tmpl in (("head_fwd", "ct_head_kernelILi%dELi1ELb0E" % r), ("head_inv", "ct_head_kernelILi%dELi0ELb1E" % r)):
+        # the power-of-two heads the LDE launches at 2^18 .. 2^23 (P2 = true; INV false / true)
+        for key, tmpl in (("head_fwd", "ct_head_kernelILi%dELi1ELb0ELb0ELb1ELb0E" % r),
+                          ("head_inv", "ct_head_kernelILi%dELi0ELb0ELb0ELb1ELb1E" % r)):
             ins = parse(kernel_lines(dis, tmpl))
             if ins:
                 v, s = straight_line(ins)
                 out.setdefault(key, {})[str(r)] = {"valu": v, "slots": s}
-    # the LDE's tails canonicalise their output (ct_tail_kernel<true>); match that one
-    # instantiation only (the name prefix alone also matches ct_tail_kernel<false>)
-    v, s = straight_line(parse(kernel_lines(dis, "ct_tail_kernelILb1E")))
+    # the LDE's tails canonicalise their output (ct_tail_kernel<true, INV>); match one
+    # instantiation each (a name prefix alone matches several)
+    v, s = straight_line(parse(kernel_lines(dis, "ct_tail_kernelILb1ELb0E")))
     out["tail"] = {"valu": v, "slots": s}
+    v, s = straight_line(parse(kernel_lines(dis, "ct_tail_kernelILb1ELb1E")))
+    out["tail_inv"] = {"valu": v, "slots": s}
     out["waves_per_block"] = 4
     out["elements_per_block"] = 8192
     return out
