@@ -91,6 +91,15 @@ __device__ __forceinline__ void ct_stage(uint64_t* x, const uint64_t* w) {
     }
 }
 
+__device__ __forceinline__ void canon4(uint64_t* x) {
+    uint32_t z0[4], z1[4];
+    glasm::canon_x4((uint32_t)x[0], (uint32_t)(x[0] >> 32), z0[0], z1[0], (uint32_t)x[1], (uint32_t)(x[1] >> 32), z0[1],
+                    z1[1], (uint32_t)x[2], (uint32_t)(x[2] >> 32), z0[2], z1[2], (uint32_t)x[3], (uint32_t)(x[3] >> 32),
+                    z0[3], z1[3]);
+#pragma unroll
+    for (int i = 0; i < 4; i++) x[i] = join2(z0[i], z1[i]);
+}
+
 __device__ __forceinline__ uint64_t canon_u64(uint64_t v) {
     uint32_t a0, a1, z0, z1;
     split2(v, a0, a1);
@@ -134,6 +143,14 @@ __device__ __forceinline__ void dft_p2_groups(uint64_t* x) {
         dft_p2<LOG, INV, (G << LOG)>(x);
         dft_p2_groups<LOG, INV, G + 1>(x);
     }
+}
+
+// the 32 factors of a prescale into registers, issued ahead of the phase that uses them (before
+// an exchange's barrier, so their latency overlaps it: the scheduler does not move loads across
+// the barrier, and after it they sat right before each product)
+__device__ __forceinline__ void load32(uint64_t* r, const uint64_t* __restrict__ f) {
+#pragma unroll
+    for (int k = 0; k < PT; k++) r[k] = f[k];
 }
 
 // x[k] *= f[k] for k < 32 (general products; outputs any u64 representative)
@@ -291,9 +308,11 @@ __global__ __launch_bounds__(NT, 2) void ct_head_kernel(uint64_t* dst, size_t ds
     }
     static_assert(!P2 || (!KAPPA && !SUB), "the power-of-two head takes whole columns, n^-1 in the tail");
     // phase A': rows s + T k, stages 0..4
+    uint64_t f[P2 ? PT : 1];
     if constexpr (P2) {
         // coefficient distance n/32 between the rows: prescale s^((n/32) k), wave-uniform
-        prescale32(x, ct + n);
+        load32(f, ct + n);
+        prescale32(x, f);
         dft_p2<5, INV, 0>(x);
     } else {
         uint64_t wa[16], wb[16];
@@ -320,13 +339,14 @@ __global__ __launch_bounds__(NT, 2) void ct_head_kernel(uint64_t* dst, size_t ds
     const uint32_t pd = 33 * W * s + w + (w >> 5);
 #pragma unroll
     for (int k = 0; k < PT; k++) lds[pa + 264 * k] = x[k];
+    if constexpr (P2 && R > 5) load32(f, ct + n + EXT_HB + 32 * s);
     __syncthreads();
 #pragma unroll
     for (int k = 0; k < PT; k++) x[k] = lds[pd + k * W + ((k * W) >> 5)];
     if constexpr (P2) {
         // rows 32 s + k: groups of 2^(R-5) rows after phase A', coefficient distance n >> R
         if constexpr (R > 5) {
-            prescale32(x, ct + n + EXT_HB + 32 * s);
+            prescale32(x, f);
             dft_p2_groups<R - 5, INV>(x);
         }
     } else {
@@ -458,41 +478,49 @@ __global__ __launch_bounds__(NT, 2) void ct_tail_kernel(uint64_t* dst, size_t ds
     uint64_t* d = dst + (size_t)blockIdx.x * dst_col_stride + (size_t)blockIdx.z * coset_stride + q * TILE;
     const uint64_t* ct = tab + (size_t)blockIdx.z * tab_stride;
     const uint64_t* ext = ct + ((size_t)1 << log_n);
-    uint64_t x[PT], wa[16], wb[16];
+    uint64_t x[PT], f[PT], wa[16], wb[16];
 #pragma unroll
     for (int k = 0; k < PT; k++) x[k] = d[t + NT * k];
-    prescale32(x, ext + EXT_TA + q * 32);
+    load32(f, ext + EXT_TA + q * 32);
+    prescale32(x, f);
     dft_p2<5, INV, 0>(x);
     const uint32_t tlo = t & 7, thi = t >> 3;
     const uint32_t ba = tail_base_a(t), bb = tail_base_b(thi, tlo), bc = tail_base_c(t);
 #pragma unroll
     for (int k = 0; k < PT; k++) lds[ba + tail_off_a(k)] = x[k];
+    load32(f, ext + ext_tb(u0) + (((q << 5) | thi) << 5));
     __syncthreads();
 #pragma unroll
     for (int k = 0; k < PT; k++) x[k] = lds[bb + tail_off_b(k)];
-    prescale32(x, ext + ext_tb(u0) + (((q << 5) | thi) << 5));
+    prescale32(x, f);
     dft_p2<5, INV, 0>(x);
+    uint64_t wc[16];
     tw_ct_tailC<10>(wa, ct, u0, q, t);
     __syncthreads();
 #pragma unroll
     for (int k = 0; k < PT; k++) lds[bb + tail_off_b(k)] = x[k];
+    // phase C's other twiddles ahead of the barrier (x is in LDS), as the prescale factors
+    tw_ct_tailC<11>(wb, ct, u0, q, t);
+    tw_ct_tailC<12>(wc, ct, u0, q, t);
     __syncthreads();
 #pragma unroll
     for (int k = 0; k < PT; k++) x[k] = lds[bc + k];
-    tw_ct_tailC<11>(wb, ct, u0, q, t);
     ct_stage<4>(x, wa);
-    tw_ct_tailC<12>(wa, ct, u0, q, t);
     ct_stage<2>(x, wb);
-    ct_stage<1>(x, wa);
+    ct_stage<1>(x, wc);
     __syncthreads();
 #pragma unroll
     for (int k = 0; k < PT; k++) lds[bc + k] = x[k];
     __syncthreads();
+    // all 32 reads first, then the canonicalisations four at a time, then the stores
 #pragma unroll
-    for (int k = 0; k < PT; k++) {
-        const uint64_t v = lds[ba + tail_off_a(k)];
-        d[t + NT * k] = CANON ? canon_u64(v) : v;
+    for (int k = 0; k < PT; k++) x[k] = lds[ba + tail_off_a(k)];
+    if constexpr (CANON) {
+#pragma unroll
+        for (int k = 0; k < PT; k += 4) canon4(x + k);
     }
+#pragma unroll
+    for (int k = 0; k < PT; k++) d[t + NT * k] = x[k];
 }
 
 // ------------------------------------------------------------ table, scale
