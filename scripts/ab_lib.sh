@@ -1,3 +1,5 @@
+# A/B of two builds of the library on one box: copy the previous build to
+# era-boojum_amd/boojum_amd/libboojum_mi355x.so.old first (it is swapped in and out).
 cd $GRAFT_REPO_ROOT && mkdir -p gpurun_out/ab && export TMPDIR=/tmp
 L=era-boojum_amd/boojum_amd/libboojum_mi355x.so
 cp $L $L.new
