@@ -271,6 +271,10 @@ __global__ __launch_bounds__(NT, 2) void ct_head_kernel(uint64_t* dst, size_t ds
     const uint32_t s = tid >> LOGW;
     const size_t o = o0 + w;
     uint64_t x[PT];
+    uint64_t f[P2 ? PT : 1];
+    // phase A' prescale factors (wave-uniform) first: after the gather's barrier they were
+    // waited for one by one
+    if constexpr (P2) load32(f, ct + n);
     if constexpr (MODE == 0) {
         // row s + T k of the tile: a wave-uniform row base (scalar) plus a per-thread 32-bit
         // index, so each load is one instruction with no address VALU
@@ -308,10 +312,8 @@ __global__ __launch_bounds__(NT, 2) void ct_head_kernel(uint64_t* dst, size_t ds
     }
     static_assert(!P2 || (!KAPPA && !SUB), "the power-of-two head takes whole columns, n^-1 in the tail");
     // phase A': rows s + T k, stages 0..4
-    uint64_t f[P2 ? PT : 1];
     if constexpr (P2) {
-        // coefficient distance n/32 between the rows: prescale s^((n/32) k), wave-uniform
-        load32(f, ct + n);
+        // coefficient distance n/32 between the rows: prescale s^((n/32) k)
         prescale32(x, f);
         dft_p2<5, INV, 0>(x);
     } else {
