@@ -235,8 +235,8 @@ __device__ __forceinline__ void head_unit(uint32_t bid, uint32_t n_cosets, bool 
 }
 
 // MODE 0: natural source; MODE 1: bit-reversed source gathered in runs of 2^R words.
-// KAPPA: multiply the stage-0 lower operands by kappa (the inverse table's CT[1] already
-// carries it for the upper ones), i.e. scale the whole transform by kappa.
+// KAPPA must be false: an inverse's n^-1 sits in its tail's TA table here (the small heads
+// still scale their own stage 0 with CT[1] + mul4_by).
 // Grid: one dimension (head_unit): with the XCD-aware placement the source tile is fetched
 // from HBM once and re-read from L2 by the other cosets.
 // SUB (log_sub > 0): stages log_sub .. log_sub + R - 1 of columns of 2^(log_n + log_sub) words
@@ -310,7 +310,8 @@ __global__ __launch_bounds__(NT, 2) void ct_head_kernel(uint64_t* dst, size_t ds
             for (int k = 0; k < PT; k++) x[k] = lds[swz_gather((s + T * k) * W + w)];
         }
     }
-    static_assert(!P2 || (!KAPPA && !SUB), "the power-of-two head takes whole columns, n^-1 in the tail");
+    static_assert(!KAPPA, "n^-1 sits in the tail's TA table (power-of-two heads) or CT[1] + the small heads");
+    static_assert(!P2 || !SUB, "the power-of-two head takes whole columns");
     // phase A': rows s + T k, stages 0..4
     if constexpr (P2) {
         // coefficient distance n/32 between the rows: prescale s^((n/32) k)
@@ -320,10 +321,6 @@ __global__ __launch_bounds__(NT, 2) void ct_head_kernel(uint64_t* dst, size_t ds
         uint64_t wa[16], wb[16];
         tw_ct_headA<0>(wa, ct, gbase);
         tw_ct_headA<1>(wb, ct, gbase);
-        if constexpr (KAPPA) {
-#pragma unroll
-            for (int k = 0; k < 16; k += 4) mul4_by(x[k], x[k + 1], x[k + 2], x[k + 3], kappa);
-        }
         ct_stage<16>(x, wa);
         tw_ct_headA<2>(wa, ct, gbase);
         ct_stage<8>(x, wb);
@@ -601,39 +598,33 @@ void launch_head_R(int mode, bool kappa_on, dim3 g, uint64_t* dst, size_t dst_co
     const dim3 g1(g.x * g.y * g.z);
     const int xcd = ((g.x * g.y) % 8) == 0 ? 1 : 0;  // units (column x tile) in whole runs of 8
     if constexpr (R >= 5) {
-        if (p2_head(log_n)) {
-            // the inverse (kappa != 0) folds n^-1 into its tail's TA table
+        // whole columns of 2^18 .. 2^23 (p2_head): the power-of-two form; an inverse (kappa != 0)
+        // has n^-1 in its tail's TA table
 #define BJ_CT_HEAD_P2(M, I)                                                                                    \
     hipLaunchKernelGGL((ct_head_kernel<R, M, false, false, true, I>), g1, dim3(NT), 0, st, dst, dst_col_stride, \
                        coset_stride, src, src_stride, log_n, tab, tab_stride, (uint64_t)0, g.z, log_tiles, xcd, \
                        0u, (size_t)0)
-            if (mode == 0) {
-                if (kappa_on) BJ_CT_HEAD_P2(0, true);
-                else BJ_CT_HEAD_P2(0, false);
-            } else {
-                if (kappa_on) BJ_CT_HEAD_P2(1, true);
-                else BJ_CT_HEAD_P2(1, false);
-            }
-#undef BJ_CT_HEAD_P2
-            return;
+        if (mode == 0) {
+            if (kappa_on) BJ_CT_HEAD_P2(0, true);
+            else BJ_CT_HEAD_P2(0, false);
+        } else {
+            if (kappa_on) BJ_CT_HEAD_P2(1, true);
+            else BJ_CT_HEAD_P2(1, false);
         }
-    }
-#define BJ_CT_HEAD(M, K)                                                                                      \
-    if constexpr (R >= 5)                                                                                     \
-        hipLaunchKernelGGL((ct_head_kernel<R, M, K>), g1, dim3(NT), 0, st, dst, dst_col_stride, coset_stride, \
-                           src, src_stride, log_n, tab, tab_stride, kappa, g.z, log_tiles, xcd, 0u,       \
-                           (size_t)0);                                                                       \
-    else                                                                                                      \
-        hipLaunchKernelGGL((ct_head_small_kernel<R, M, K>), g1, dim3(NT), 0, st, dst, dst_col_stride,         \
-                           coset_stride, src, src_stride, log_n, tab, tab_stride, kappa, g.z, log_tiles, xcd)
-    if (mode == 0) {
-        if (kappa_on) BJ_CT_HEAD(0, true);
-        else BJ_CT_HEAD(0, false);
+#undef BJ_CT_HEAD_P2
     } else {
-        if (kappa_on) BJ_CT_HEAD(1, true);
-        else BJ_CT_HEAD(1, false);
-    }
+#define BJ_CT_HEAD(M, K)                                                                                 \
+    hipLaunchKernelGGL((ct_head_small_kernel<R, M, K>), g1, dim3(NT), 0, st, dst, dst_col_stride, coset_stride, \
+                       src, src_stride, log_n, tab, tab_stride, kappa, g.z, log_tiles, xcd)
+        if (mode == 0) {
+            if (kappa_on) BJ_CT_HEAD(0, true);
+            else BJ_CT_HEAD(0, false);
+        } else {
+            if (kappa_on) BJ_CT_HEAD(1, true);
+            else BJ_CT_HEAD(1, false);
+        }
 #undef BJ_CT_HEAD
+    }
 }
 
 }  // namespace

@@ -10,7 +10,7 @@ import os
 import sys
 
 
-def run(rank, world, port, cfg, outdir, device, paths):
+def run(rank, world, cfg, outdir, device, paths):
     for p in paths:
         if p not in sys.path:
             sys.path.insert(0, p)
@@ -18,9 +18,9 @@ def run(rank, world, port, cfg, outdir, device, paths):
     import torch
     import torch.distributed as dist
 
-    os.environ["MASTER_ADDR"] = "127.0.0.1"
-    os.environ["MASTER_PORT"] = str(port)
-    dist.init_process_group("gloo", rank=rank, world_size=world)
+    # rendezvous through a file in the test's own directory: no TCP port to collide with
+    dist.init_process_group("gloo", init_method="file://" + os.path.join(outdir, "rendezvous"), rank=rank,
+                            world_size=world)
     try:
         n_cols, log_n, log_lde, cap = cfg[:4]
         hasher = cfg[6] if len(cfg) > 6 and cfg[6] else "poseidon2"

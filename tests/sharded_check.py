@@ -1,7 +1,6 @@
 """Launch a G-rank sharded commit (gloo) and check every rank's outputs against the oracle's
 single-process commit of the same synthetic trace.  Shared by the CPU and GPU tests."""
 import os
-import socket
 
 import numpy as np
 
@@ -12,16 +11,10 @@ ROOT = os.path.dirname(HERE)
 PATHS = [HERE, ROOT, os.path.join(ROOT, "era-boojum_amd"), os.path.join(ROOT, "oracle")]
 
 
-def free_port():
-    with socket.socket() as s:
-        s.bind(("127.0.0.1", 0))
-        return s.getsockname()[1]
-
-
 def run_and_check(world, cfg, tmp_path, device):
     import torch.multiprocessing as mp
     import shard_worker
-    mp.start_processes(shard_worker.run, args=(world, free_port(), cfg, str(tmp_path), device, PATHS), nprocs=world,
+    mp.start_processes(shard_worker.run, args=(world, cfg, str(tmp_path), device, PATHS), nprocs=world,
                        join=True, start_method="spawn")
     n_cols, log_n, log_lde, cap = cfg[:4]
     hasher = cfg[6] if len(cfg) > 6 and cfg[6] else "poseidon2"
