@@ -1,4 +1,4 @@
-// Coset-folded Cooley-Tukey NTT passes for 2^13 <= n <= 2^23.
+// Coset-folded Cooley-Tukey NTT passes for 2^13 <= n <= 2^26.
 //
 // The reference's transform is serial_ct_ntt_natural_to_bitreversed (fft/mod.rs:659-734):
 // at the stage with 2^u groups, group k pairs (j, j + h) and does
@@ -12,9 +12,14 @@
 // bit-identical to the reference's.
 //
 // Twiddle table per shift: CT[2^u + k] = mu_k(s), for u < log n, k < 2^u (n entries, CT[0]
-// unused). The inverse table (w^-1, s = 1) carries n^-1 in CT[1], and the head kernel
-// multiplies the stage-0 lower operands by n^-1 as well, so the inverse transform returns
-// the monomials themselves (utils.rs:295-304 after ifft's x n^-1), not n * monomials.
+// unused), followed by the prescale tables of the power-of-two register phases (below). The
+// inverse transform returns the monomials themselves (utils.rs:295-304 after ifft's x n^-1),
+// not n * monomials: n^-1 sits in the tail's TA table (2^13, 2^18..2^23), or in CT[1] with the
+// general heads multiplying their stage-0 lower operands by it.
+//
+// Register phases of <= 5 stages (the tail's A and B, the 2^18..2^23 heads' A' and B') run as
+// a prescale by powers of the group's coset shift and a DFT with twiddles +-2^e
+// (csrc/ntt_pow2.hpp); the tail's phase C and the other heads keep mu_k(s).
 //
 // Tiling: each thread holds 32 elements in VGPRs and runs up to five
 // stages in registers; LDS (XOR-swizzled) only re-deals elements between register phases.
