@@ -50,7 +50,9 @@ uint32_t bj_abi_version(void);
 
 /* Fill the device twiddle cache for FFT size 2^log_n (forward + inverse tables) on the
  * current device, synchronously.  Twiddle precompute is outside the timed region in
- * the reference's own accounting (prover.rs:313-353 precomputes before "LDE taken"). */
+ * the reference's own accounting (prover.rs:313-353 precomputes before "LDE taken").
+ * Cached tables are never freed; for 2^13 <= n <= 2^26 a table of one coset shift is
+ * n + 1056 (1 + n / 2^13) u64 (36 MiB at 2^22), and an LDE at degree D keeps D of them. */
 int bj_prepare(uint32_t log_n);
 
 /* ---------------------------------------------------------------- FFT seam */
