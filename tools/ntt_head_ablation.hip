@@ -1,14 +1,15 @@
 // Where the forward CT head's time goes (csrc/ntt_ct.hip, ct_head_kernel<9, 1, false>: the first 9
 // stages of C3's four coset transforms, gathering the bit-reversed monomials), next to copies
-// with one part removed at a time; the same method as tools/ntt_tail_ablation.hip.  Results
-// are garbage for the ablated variants: only the time matters.  DESIGN.md section 4.2.
+// with one part removed at a time.  Results are garbage for the ablated variants: only the
+// time matters.  DESIGN.md section 4.2.  This is the general-twiddle head of round 2's first
+// half; C3 now runs the power-of-two form (ct_head_kernel<9, 1, false, false, true>, section 4.3).
 //   0 full                 the production kernel's sequence
 //   1 no global load       x from registers (thread id), no gather, no staging exchange
 //   2 no store             results feed one predicated store (never taken)
 //   3 no LDS               gather staging and the A'->B' exchange removed (loads kept)
 //   4 no twiddle loads     twiddles from registers
 //   5 butterflies only     1 + 2 + 3 + 4
-//   6 the production kernel as it now stands (variant 0 is the sequence this tool copied)
+//   6 the general head as it now stands in ntt_ct.hip (variant 0 is the sequence this tool copied)
 // Build: hipcc -O3 -std=c++17 --offload-arch=gfx950 -I era-boojum_amd/csrc -o tools/ntt_head_ablation tools/ntt_head_ablation.hip
 #include "../era-boojum_amd/csrc/ntt_ct.hip"
 #include <cstdio>
