@@ -112,7 +112,8 @@ class NativeComm:
         """The callback transport over a torch.distributed group of any backend (gloo for ranks
         that share a GPU): the library stages each exchange through host memory and this callback
         runs it as a torch collective on CPU tensors.  Every exchange synchronises, so this is a
-        rehearsal transport (correctness of the N > 1 pipeline on one card), not a benchmark."""
+        rehearsal transport (correctness of the N > 1 pipeline on one card), not a benchmark.  A
+        failing exchange aborts the group, so the peers' calls fail promptly too."""
         import torch.distributed as dist
         world, rank = dist.get_world_size(group), dist.get_rank(group)
 
@@ -129,6 +130,12 @@ class NativeComm:
             except Exception:  # noqa: BLE001 - reported through the C return code
                 import traceback
                 traceback.print_exc()
+                # the peers are blocked in the same collective: abort the group so they fail
+                # now (gloo: "connection closed by peer") instead of at the group's timeout
+                try:
+                    (group if group is not None else dist.group.WORLD).abort()
+                except Exception:  # noqa: BLE001 - best effort; the error is returned either way
+                    pass
                 return 1
 
         fn = _EXCHANGE_FN(exchange)

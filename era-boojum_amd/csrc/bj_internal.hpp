@@ -99,6 +99,7 @@ int set_error(int code, const char* msg);
 // capi.hip: stream-ordered allocation from the library's private pool of the current device
 // (free with hipFreeAsync); the process's default pool is never reconfigured
 hipError_t pool_alloc(void** p, size_t bytes, hipStream_t st);
+hipError_t pool_trim_all();
 // capi.hip: LDE coset shift 7 * w_{nD}^{bitrev_{log D}(i)} (utils.rs:334-347, 370-373) and the
 // shift of leaf range `shard` of 2^log_shards over the n*D domain, 7 * w_{nD}^{bitrev(shard)}
 uint64_t shard_shift(uint32_t log_n, uint32_t log_lde, uint32_t log_shards, uint32_t shard);

@@ -357,9 +357,21 @@ uint64_t shard_shift(uint32_t log_n, uint32_t log_lde, uint32_t log_shards, uint
 // alone (its release threshold belongs to the host application); ours keeps freed memory
 // mapped between calls, so a repeated commit does not re-map its workspace after every
 // synchronisation (~20 ms for C2's 5 GB).
+static std::mutex g_pool_mu;
+static std::map<int, hipMemPool_t>* g_pools = new std::map<int, hipMemPool_t>();
+
+hipError_t pool_trim_all() {
+    std::lock_guard<std::mutex> lk(g_pool_mu);
+    for (auto& kv : *g_pools) {
+        hipError_t e = hipMemPoolTrimTo(kv.second, 0);
+        if (e != hipSuccess) return e;
+    }
+    return hipSuccess;
+}
+
 hipError_t pool_alloc(void** p, size_t bytes, hipStream_t st) {
-    static std::mutex mu;
-    static std::map<int, hipMemPool_t>* pools = new std::map<int, hipMemPool_t>();
+    std::mutex& mu = g_pool_mu;
+    std::map<int, hipMemPool_t>* pools = g_pools;
     int dev = 0;
     hipError_t e = hipGetDevice(&dev);
     if (e != hipSuccess) return e;
@@ -390,7 +402,12 @@ hipError_t pool_alloc(void** p, size_t bytes, hipStream_t st) {
 extern "C" {
 
 const char* bj_last_error(void) { return g_err.c_str(); }
-uint32_t bj_abi_version(void) { return (2u << 16) | 0u; }
+uint32_t bj_abi_version(void) { return (2u << 16) | 1u; }
+
+int bj_release_workspace(void) {
+    HIP_TRY(bj::pool_trim_all(), "hipMemPoolTrimTo");
+    return BJ_OK;
+}
 
 int bj_prepare(uint32_t log_n) {
     if (int r = check_log_n(log_n)) return r;

@@ -156,10 +156,35 @@ struct bj_comm {
         int phase;
     };
     std::vector<Interval> intervals;
+    float folded_ms[4] = {0, 0, 0, 0};  // intervals already completed and summed
     int timed_calls = 0;
 };
 
 namespace {
+
+// Sum the intervals whose end event has completed into folded_ms and free their events (all of
+// them when `wait`).  Called at the start of every commit, so a caller that times calls and never
+// reads the totals holds the events of its in-flight calls only.
+int fold_intervals(bj_comm* c, bool wait) {
+    int rc = BJ_OK;
+    size_t keep = 0;
+    for (size_t i = 0; i < c->intervals.size(); i++) {
+        const bj_comm::Interval iv = c->intervals[i];
+        hipError_t e = wait ? hipEventSynchronize(iv.b) : hipEventQuery(iv.b);
+        if (e == hipErrorNotReady) {
+            c->intervals[keep++] = iv;
+            continue;
+        }
+        float ms = 0;
+        if (e == hipSuccess) e = hipEventElapsedTime(&ms, iv.a, iv.b);
+        if (e != hipSuccess && rc == BJ_OK) rc = err(BJ_EHIP, std::string("phase timing: ") + hipGetErrorString(e));
+        if (iv.phase >= 0 && iv.phase < 4) c->folded_ms[iv.phase] += ms;
+        (void)hipEventDestroy(iv.a);
+        (void)hipEventDestroy(iv.b);
+    }
+    c->intervals.resize(keep);
+    return rc;
+}
 
 // Phase intervals of one timed call (bj_comm_set_timing); a no-op when timing is off.
 struct PhaseTimer {
@@ -513,19 +538,11 @@ int bj_comm_set_timing(bj_comm* c, int on) {
 
 int bj_comm_phase_ms(bj_comm* c, float* ms_out4, int* calls_out) {
     if (!c || !ms_out4) return err(BJ_EINVAL, "null argument");
-    float acc[4] = {0, 0, 0, 0};
-    int rc = BJ_OK;
-    for (const bj_comm::Interval& iv : c->intervals) {
-        float ms = 0;
-        hipError_t e = hipEventSynchronize(iv.b);
-        if (e == hipSuccess) e = hipEventElapsedTime(&ms, iv.a, iv.b);
-        if (e != hipSuccess && rc == BJ_OK) rc = err(BJ_EHIP, std::string("phase timing: ") + hipGetErrorString(e));
-        if (iv.phase >= 0 && iv.phase < 4) acc[iv.phase] += ms;
-        (void)hipEventDestroy(iv.a);
-        (void)hipEventDestroy(iv.b);
+    int rc = fold_intervals(c, true);
+    for (int i = 0; i < 4; i++) {
+        ms_out4[i] = c->folded_ms[i];
+        c->folded_ms[i] = 0;
     }
-    c->intervals.clear();
-    for (int i = 0; i < 4; i++) ms_out4[i] = acc[i];
     if (calls_out) *calls_out = c->timed_calls;
     c->timed_calls = 0;
     return rc;
@@ -625,6 +642,7 @@ int bj_sharded_commit_d(bj_comm* comm, const uint64_t* trace_shard, size_t trace
     }
     std::vector<uint64_t> spm(world);
     // phases 0 inverse (+ fold), 1 lde, 2 leaves, 3 nodes (bj_comm_set_timing)
+    if (!comm->intervals.empty()) BJ_CHECK(fold_intervals(comm, false));
     PhaseTimer pt(comm, st);
 
     // 1. local inverse transforms (and folds), each chunk's exchange issued as soon as its

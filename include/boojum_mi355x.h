@@ -55,6 +55,17 @@ uint32_t bj_abi_version(void);
  * n + 1056 (1 + n / 2^13) u64 (36 MiB at 2^22), and an LDE at degree D keeps D of them. */
 int bj_prepare(uint32_t log_n);
 
+/* Return the library's cached device workspace to the system (ABI 2.1; no reference
+ * counterpart: the reference's Vec workspaces are freed when dropped).  The *_h calls, the
+ * host-buffer commit, the collective commit and the LDE's own temporaries take their device
+ * workspace from a stream-ordered pool private to the library (one per device); freed blocks
+ * stay mapped for the next call (re-mapping C2's 5 GB after every call cost ~20 ms), so after a
+ * large call the pool keeps that much reserved -- e.g. ~8.5 GB after a native C3 commit at N = 1.
+ * This trims every device's pool to the blocks still in use (hipMemPoolTrimTo(pool, 0)); blocks
+ * whose stream-ordered free has not completed yet are released by a later call.  Call it when a
+ * long-running prover goes idle.  Twiddle tables (bj_prepare) are not affected. */
+int bj_release_workspace(void);
+
 /* ---------------------------------------------------------------- FFT seam */
 
 /* precompute_twiddles_for_fft::<INVERSED> (cs/implementations/utils.rs:88-125,
@@ -318,9 +329,11 @@ int bj_comm_exchange_d(bj_comm* comm, int kind, const void* send, void* recv, si
  * reference logs its phase times, merkle_tree.rs:162-167, prover.rs:345).  on != 0: every later
  * call records HIP events on its compute stream around the inverse transforms (+ folds), the
  * LDE evaluations, the leaf hashing and the subtree + cap; waits for the exchange are outside
- * every interval.  bj_comm_phase_ms waits for the recorded calls, writes the summed
- * milliseconds {inverse, lde, leaves, nodes} to ms_out[4] and their count to *calls_out, and
- * starts a new sum. */
+ * every interval.  Each call first sums the intervals of earlier calls that have completed and
+ * frees their events, so the events held are those of calls still in flight.  bj_comm_phase_ms
+ * waits for the recorded calls, writes the summed milliseconds {inverse, lde, leaves, nodes} to
+ * ms_out[4] and their count to *calls_out, and starts a new sum.  The events cost a little time
+ * on the compute stream: time production steps with timing off. */
 int bj_comm_set_timing(bj_comm* comm, int on);
 int bj_comm_phase_ms(bj_comm* comm, float* ms_out4, int* calls_out);
 

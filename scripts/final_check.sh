@@ -14,5 +14,5 @@ timeout -k 10 300 python -m torch.distributed.run --nnodes=1 --nproc-per-node 2 
 grep '"metric"' $O/torchrun2_C2.log | cut -c1-200
 timeout -k 10 300 python -u bench.py --gpus 4 --dist-backend gloo --config C2 --steps 2 --warmup 1 > $O/self4_C2.log 2>&1 || { echo "self-launch x4 failed"; tail -20 $O/self4_C2.log; exit 1; }
 grep '"metric"' $O/self4_C2.log | cut -c1-200
-timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d $O/trace -o run -- python3 bench.py --steps 3 --warmup 1 --no-cpu-baseline > $O/trace.log 2>&1 || { echo "trace failed"; exit 1; }
+timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d $O/trace -o run -- python3 bench.py --steps 3 --warmup 1 --no-cpu-baseline --no-native-base > $O/trace.log 2>&1 || { echo "trace failed"; exit 1; }
 echo done

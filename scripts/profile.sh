@@ -12,7 +12,7 @@ OUT=gpurun_out/prof_$TAG
 mkdir -p $OUT
 timeout -k 10 400 python3 bench.py > $OUT/bench_default.log 2>&1 || { echo "bench rc=$?"; tail -5 $OUT/bench_default.log; exit 1; }
 tail -1 $OUT/bench_default.log
-B="python3 bench.py --config C3 --no-cpu-baseline"
+B="python3 bench.py --config C3 --no-cpu-baseline --no-native-base"
 timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d $OUT/trace -o run -- $B --steps 3 --warmup 1 > $OUT/trace.log 2>&1 || { echo "trace rc=$?"; tail -5 $OUT/trace.log; exit 1; }
 echo trace ok
 timeout -s KILL 240 rocprofv3 --pmc FETCH_SIZE --output-format csv -d $OUT/fetch -o run -- $B --steps 1 --warmup 0 > $OUT/fetch.log 2>&1 || { echo "fetch rc=$?"; tail -5 $OUT/fetch.log; exit 1; }

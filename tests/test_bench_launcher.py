@@ -2,6 +2,7 @@
 never touches a GPU) and returns the first failing rank's exit code after stopping the others.
 On a machine without a GPU every rank fails at its device selection, which exercises exactly
 that failure path: the parent must return non-zero promptly, not hang."""
+import json
 import os
 import subprocess
 import sys
@@ -30,3 +31,47 @@ def test_rank_count_must_match_world_size():
     r = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), "--gpus", "4", "--config", "C1"], env=env,
                        capture_output=True, text=True, timeout=240)
     assert r.returncode != 0 and "WORLD_SIZE=2" in (r.stderr + r.stdout)
+
+
+def _bench(args, **env_extra):
+    env = {k: v for k, v in os.environ.items() if k not in ("WORLD_SIZE", "RANK", "LOCAL_RANK", "MASTER_PORT")}
+    env.update(env_extra)
+    return subprocess.Popen([sys.executable, os.path.join(ROOT, "bench.py")] + args, env=env, stdout=subprocess.PIPE,
+                            stderr=subprocess.PIPE, text=True)
+
+
+def test_hung_rank_ends_the_job_inside_the_deadline():
+    """A rank that never reaches its rendezvous: the parent's deadline stops every rank (SIGTERM,
+    then SIGKILL) and prints one JSON error line naming the ranks alive and their last phases."""
+    t0 = time.time()
+    p = _bench(["--gpus", "2", "--launch-check", "--timeout", "15"], BJ_BENCH_TEST_HANG_RANK="1")
+    out, err = p.communicate(timeout=120)
+    elapsed = time.time() - t0
+    assert p.returncode == 124, (out, err)
+    line = json.loads(out.strip().splitlines()[-1])
+    assert "deadline" in line["error"]
+    assert line["ranks_alive"] == [0, 1]
+    assert line["last_phase"]["1"] == "test-hang"
+    assert line["last_phase"]["0"] == "init"
+    assert 15 <= elapsed < 60
+
+
+def test_two_self_launched_jobs_do_not_collide():
+    """Two 4-rank jobs started together on one host rendezvous through their own file stores."""
+    jobs = [_bench(["--gpus", "4", "--launch-check", "--timeout", "120"]) for _ in range(2)]
+    for p in jobs:
+        out, err = p.communicate(timeout=180)
+        assert p.returncode == 0, err
+        line = json.loads(out.strip().splitlines()[-1])
+        assert line == {"launch_check": "ok", "n_gpus": 4, "rank_sum": 10, "rendezvous": "file"}
+
+
+def test_rank_watchdog_under_an_external_launcher():
+    """Under torchrun-style env (no parent deadline) a hung rank still ends itself (exit 124)."""
+    env = dict(os.environ, WORLD_SIZE="1", RANK="0", LOCAL_RANK="0", BJ_BENCH_TEST_HANG_RANK="0")
+    env.pop("BJ_BENCH_INIT", None)
+    t0 = time.time()
+    r = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), "--launch-check", "--timeout", "5"], env=env,
+                       capture_output=True, text=True, timeout=120)
+    assert r.returncode == 124 and "deadline passed in phase 'test-hang'" in r.stderr
+    assert time.time() - t0 < 60

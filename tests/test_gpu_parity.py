@@ -418,6 +418,29 @@ def test_commit_host_abi_matches(bj, c, log_n, log_d, cap, log_k):
     eq(capo, ref["cap"])
 
 
+def test_release_workspace_between_host_commits(bj):
+    """bj_release_workspace (ABI 2.1) trims the library's pool after a host commit; the next
+    commit re-allocates its workspace and is still bit-exact."""
+    import ctypes
+    from boojum_amd._lib import call, load
+    assert load().bj_abi_version() == (2 << 16) | 1
+    c, log_n, log_d, cap = 40, 14, 2, 16
+    tr = O.synthetic_trace(c, log_n)
+    ref = O.lde_commit(tr, log_d, cap, threads=8)
+    p = lambda a: a.ctypes.data_as(ctypes.POINTER(ctypes.c_uint64))  # noqa: E731
+    for _ in range(2):
+        nl = 1 << (log_n + log_d)
+        lde = np.zeros((c, 1 << log_d, 1 << log_n), dtype=np.uint64)
+        leaves = np.zeros((nl, 4), dtype=np.uint64)
+        nodes = np.zeros((nl - cap, 4), dtype=np.uint64)
+        capo = np.zeros((cap, 4), dtype=np.uint64)
+        call("bj_lde_commit_h", p(np.ascontiguousarray(tr)), c, log_n, log_d, log_d, cap, p(lde), p(leaves),
+             p(nodes), p(capo))
+        call("bj_release_workspace")
+        eq(lde, ref["lde"])
+        eq(capo, ref["cap"])
+
+
 def test_errors_are_loud(bj):
     from boojum_amd import BoojumError
     t = bj.torch.zeros((2, 24), dtype=bj.torch.int64, device="cuda")

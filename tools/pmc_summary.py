@@ -21,6 +21,7 @@ import collections
 import csv
 import json
 import os
+import sys
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 
@@ -75,10 +76,16 @@ def main():
             for c, vals in ctrs.items():
                 d[c] = sum(vals) / len(vals)
                 d[c + "_dispatches"] = len(vals)
+    # the source hashes of the library the passes ran (build_info.json, written by build()):
+    # bench.py quotes an entry only while the built library's hash for its group is the same
+    sys.path.insert(0, os.path.join(ROOT, "era-boojum_amd"))
+    from boojum_amd import srchash
+    info = os.path.join(ROOT, "era-boojum_amd", "boojum_amd", "build_info.json")
+    hashes = json.load(open(info))["src_hash"] if os.path.exists(info) else srchash.source_hashes()
     out = {}
     for k, d in data.items():
         fac = next(f for _, kk, f in KERNELS if kk == k)
-        e = {"source": os.path.basename(os.path.normpath(args.dir))}
+        e = {"source": os.path.basename(os.path.normpath(args.dir)), "src_hash": hashes.get(srchash.group_of(k))}
         if "FETCH_SIZE" in d:
             e["fetch_bytes"] = d["FETCH_SIZE"] * 1024 * fac
         if "WRITE_SIZE" in d:
@@ -94,7 +101,8 @@ def main():
     ct = [out.get(k) for k in ("ct_head_inv", "ct_head_fwd", "ct_tail")]
     if all(x and "hbm_bytes_per_launch" in x for x in ct):
         out["lde"] = {"hbm_bytes_per_launch": ct[0]["hbm_bytes_per_launch"] + ct[1]["hbm_bytes_per_launch"]
-                      + 2 * ct[2]["hbm_bytes_per_launch"], "note": "iNTT + forward, one commit"}
+                      + 2 * ct[2]["hbm_bytes_per_launch"], "note": "iNTT + forward, one commit",
+                      "src_hash": hashes.get("lde")}
     full = {}
     if os.path.exists(args.out):
         full = json.load(open(args.out))
