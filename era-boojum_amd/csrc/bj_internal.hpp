@@ -84,6 +84,21 @@ hipError_t launch_ct(uint64_t* dst, size_t dst_col_stride, size_t coset_stride, 
                      const uint64_t* src, size_t src_stride, bool src_bitrev, uint32_t n_cols, uint32_t log_n,
                      const uint64_t* tab, size_t tab_stride, uint64_t kappa, bool canon_out, hipStream_t st);
 hipError_t launch_scale(uint64_t* cols, size_t stride, uint32_t n_cols, size_t n, uint64_t k, hipStream_t st);
+hipError_t launch_ct_inverse_head(uint64_t* dst, size_t dst_col_stride, const uint64_t* src, size_t src_stride,
+                                  uint32_t n_cols, uint32_t log_n, const uint64_t* inv_tab, hipStream_t st);
+
+// ntt_lde3.hip: the three-pass LDE for 2^18 <= n <= 2^23 (inverse head; inverse tail fused with
+// the first 13 forward stages of every coset; the last log n - 13 forward stages)
+bool lde3_supported(uint32_t log_n);
+size_t lde3_table_len(uint32_t log_n);
+hipError_t launch_lde3_table(uint64_t* out, uint32_t log_n, uint64_t shift, hipStream_t st);
+// middle + final passes.  src: inv_tab != NULL -> the inverse head's output (natural order after
+// its log n - 13 stages), and mono (if non-NULL) receives the canonical monomials in bit-reversed
+// order; inv_tab == NULL -> src holds the monomials in bit-reversed order already.  Output coset
+// i (table tabs + i * tab_stride) of column c at lde + c * col_stride + i * coset_stride.
+hipError_t launch_lde3(uint64_t* lde, size_t col_stride, size_t coset_stride, uint32_t n_cosets, const uint64_t* src,
+                       size_t src_stride, uint64_t* mono, size_t mono_stride, uint32_t n_cols, uint32_t log_n,
+                       const uint64_t* inv_tab, const uint64_t* tabs, size_t tab_stride, hipStream_t st);
 }  // namespace bj
 
 namespace bj {

@@ -8,6 +8,7 @@
 #include <tuple>
 #include <vector>
 #include <cstring>
+#include <cstdlib>
 #include <cstdio>
 #include <algorithm>
 #include <thread>
@@ -51,6 +52,8 @@ struct Cache {
     std::map<std::tuple<int, uint32_t, uint32_t, int>, uint64_t*> lde_pw;
     std::map<std::tuple<int, uint32_t, int, uint64_t>, uint64_t*> ct;
     std::map<std::tuple<int, uint32_t, uint32_t>, uint64_t*> ct_lde;
+    std::map<std::tuple<int, uint32_t, uint64_t>, uint64_t*> lde3;
+    std::map<std::tuple<int, uint32_t, uint32_t>, uint64_t*> lde3_lde;
 };
 Cache& cache() {
     static Cache* c = new Cache();
@@ -209,6 +212,64 @@ int get_ct_lde(uint32_t log_n, uint32_t log_d, const uint64_t** out) {
     return BJ_OK;
 }
 
+// Three-pass LDE tables (ntt_lde3.hip) of one shift, and of the D coset shifts of an LDE (table i
+// at out + i * lde3_table_len).
+int get_lde3(uint32_t log_n, uint64_t shift_, const uint64_t** out) {
+    int dev = 0;
+    HIP_TRY(hipGetDevice(&dev), "hipGetDevice");
+    const uint64_t shift = gl::canon(shift_);
+    Cache& c = cache();
+    std::lock_guard<std::mutex> lk(c.mu);
+    auto key = std::make_tuple(dev, log_n, shift);
+    auto it = c.lde3.find(key);
+    if (it != c.lde3.end()) { *out = it->second; return BJ_OK; }
+    uint64_t* p = nullptr;
+    HIP_TRY(hipMalloc(&p, bj::lde3_table_len(log_n) * sizeof(uint64_t)), "hipMalloc(lde3 table)");
+    hipStream_t st;
+    HIP_TRY(hipStreamCreateWithFlags(&st, hipStreamNonBlocking), "hipStreamCreate");
+    hipError_t e = bj::launch_lde3_table(p, log_n, shift, st);
+    if (e == hipSuccess) e = hipStreamSynchronize(st);
+    (void)hipStreamDestroy(st);
+    if (e != hipSuccess) { (void)hipFree(p); return hip_fail(e, "lde3 table"); }
+    c.lde3[key] = p;
+    *out = p;
+    return BJ_OK;
+}
+
+uint64_t lde_coset(uint32_t log_n, uint32_t log_d, uint32_t i);
+
+int get_lde3_lde(uint32_t log_n, uint32_t log_d, const uint64_t** out) {
+    int dev = 0;
+    HIP_TRY(hipGetDevice(&dev), "hipGetDevice");
+    Cache& c = cache();
+    std::lock_guard<std::mutex> lk(c.mu);
+    auto key = std::make_tuple(dev, log_n, log_d);
+    auto it = c.lde3_lde.find(key);
+    if (it != c.lde3_lde.end()) { *out = it->second; return BJ_OK; }
+    const size_t L = bj::lde3_table_len(log_n);
+    const uint32_t D = 1u << log_d;
+    uint64_t* p = nullptr;
+    HIP_TRY(hipMalloc(&p, D * L * sizeof(uint64_t)), "hipMalloc(lde3 lde tables)");
+    hipStream_t st;
+    HIP_TRY(hipStreamCreateWithFlags(&st, hipStreamNonBlocking), "hipStreamCreate");
+    hipError_t e = hipSuccess;
+    for (uint32_t i = 0; i < D && e == hipSuccess; i++)
+        e = bj::launch_lde3_table(p + i * L, log_n, lde_coset(log_n, log_d, i), st);
+    if (e == hipSuccess) e = hipStreamSynchronize(st);
+    (void)hipStreamDestroy(st);
+    if (e != hipSuccess) { (void)hipFree(p); return hip_fail(e, "lde3 lde tables"); }
+    c.lde3_lde[key] = p;
+    *out = p;
+    return BJ_OK;
+}
+
+// The three-pass LDE (ntt_lde3.hip) is the default for 2^18..2^23; BJ_LDE_PASSES=2 selects the
+// two-pass CT path (head + tail per transform) instead, for same-binary A/B measurements.
+bool use_lde3(uint32_t log_n) {
+    const char* v = getenv("BJ_LDE_PASSES");
+    return !(v && v[0] == '2') && bj::lde3_supported(log_n);
+}
+
 inline bool is_pow2(size_t x) { return x && !(x & (x - 1)); }
 
 int log2_exact(size_t len, uint32_t* out) {
@@ -290,6 +351,16 @@ int lde_forward(uint64_t* lde, size_t col_stride, size_t coset_stride, uint32_t 
                 const uint64_t* src, size_t src_stride, bool src_bitrev, uint32_t n_cols, uint32_t log_n,
                 uint32_t log_lde, hipStream_t st) {
     const size_t n = (size_t)1 << log_n;
+    if (src_bitrev && use_lde3(log_n)) {
+        // forward stages 0..12 of every coset from each bit-reversed block, then the last log n - 13
+        const uint64_t* tabs;
+        if (int r = get_lde3_lde(log_n, log_lde, &tabs)) return r;
+        const size_t L = bj::lde3_table_len(log_n);
+        HIP_TRY(bj::launch_lde3(lde, col_stride, coset_stride, n_cosets, src, src_stride, nullptr, 0, n_cols, log_n,
+                                nullptr, tabs + (size_t)first * L, L, st),
+                "coset fft");
+        return BJ_OK;
+    }
     if (bj::ct_ntt_supported(log_n)) {
         const uint64_t* tabs;
         if (int r = get_ct_lde(log_n, log_lde, &tabs)) return r;
@@ -329,6 +400,13 @@ int check_shards(uint32_t log_n, uint32_t log_lde, uint32_t log_shards) {
 int shard_from_folded(const uint64_t* folded, size_t folded_stride, uint32_t n_cols, uint32_t log_m, uint64_t sp,
                       uint64_t* lde, hipStream_t st) {
     const size_t m = (size_t)1 << log_m;
+    if (use_lde3(log_m)) {
+        const uint64_t* tab;
+        if (int r = get_lde3(log_m, sp, &tab)) return r;
+        HIP_TRY(bj::launch_lde3(lde, m, 0, 1, folded, folded_stride, nullptr, 0, n_cols, log_m, nullptr, tab, 0, st),
+                "coset fft");
+        return BJ_OK;
+    }
     if (bj::ct_ntt_supported(log_m)) {
         const uint64_t* tab;
         if (int r = get_ct(log_m, false, sp, &tab)) return r;
@@ -527,6 +605,19 @@ int bj_lde_d(const uint64_t* trace, uint32_t n_cols, size_t trace_stride, uint32
     if (n_cols == 0) return BJ_OK;
     const size_t n = (size_t)1 << log_n;
     const uint32_t D = 1u << log_lde;
+    if (use_lde3(log_n)) {
+        // three passes (ntt_lde3.hip): the inverse head into scratch; the inverse tail fused with
+        // forward stages 0..12 of all D cosets (the canonical monomials left in scratch, c_j at
+        // bitrev_n(j)); the last log n - 13 forward stages in place on the LDE
+        const uint64_t *inv, *tabs;
+        if (int r = get_ct(log_n, true, 1, &inv)) return r;
+        if (int r = get_lde3_lde(log_n, log_lde, &tabs)) return r;
+        HIP_TRY(bj::launch_ct_inverse_head(scratch, n, trace, trace_stride, n_cols, log_n, inv, S(stream)), "ifft");
+        HIP_TRY(bj::launch_lde3(lde, (size_t)D * n, n, D, scratch, n, scratch, n, n_cols, log_n, inv, tabs,
+                                bj::lde3_table_len(log_n), S(stream)),
+                "lde");
+        return BJ_OK;
+    }
     // iFFT (utils.rs:295-304): scratch = monomials in bit-reversed order; the forward pass
     // gathers them back in natural order, all D cosets (utils.rs:363-379).
     if (int r = inverse_to_bitrev(scratch, n, trace, trace_stride, n_cols, log_n, S(stream))) return r;

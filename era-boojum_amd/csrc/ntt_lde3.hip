@@ -1,0 +1,534 @@
+// Three-pass coset LDE for 2^18 <= n <= 2^23 (R = log n - 13 = 5..10).
+//
+// The reference computes D coset FFTs of the same monomials (transform_monomials_to_lde,
+// cs/implementations/utils.rs:311-403): per coset distribute_powers + the natural->bit-reversed
+// CT network (fft/mod.rs:308-317, 659-734).  The two-pass form (ntt_ct.hip) runs every transform
+// as a head of R stages and a tail of 13; the inverse tail writes the monomials, and the forward
+// head gathers them back once per coset.  Here the inverse tail and the first 13 stages of all D
+// forward transforms share one block:
+//
+//   block q of the inverse tail (positions [8192 q, 8192 (q+1)) of the bit-reversed monomial
+//   array) holds c_j for j = bitrev_13(l) 2^R + bitrev_R(q), l < 8192: every j with the same low
+//   R bits, and the forward network's stages 0..12 (pair distances 2^(log n - 1) .. 2^R) only
+//   ever pair such j.  So one block runs the inverse's last 13 stages, keeps the monomials in
+//   registers, and for each coset runs forward stages 0..12 on them.
+//
+// Pass 1  inverse head (ntt_ct.hip, launch_ct_inverse_head): trace -> scratch.
+// Pass 2  lde3_mid_kernel: scratch block q -> inverse stages R..R+12 -> (optionally the canonical
+//         monomials back to scratch: bj_lde_d's contract) -> per coset: forward stages 0..12
+//         (phases A, B in the power-of-two form, C general) -> 2^R runs of W = 2^(13-R) words,
+//         run T of block q written to [T 8192 + q W, + W) of the coset's column.
+// Pass 3  lde3_final_kernel: region T (8192 contiguous words: rows q < 2^R of W values M =
+//         T W + o) -> the last R forward stages on each M's 2^R values (rows in bit-reversed
+//         order: r = bitrev_R(q)) -> the region in natural order, o 2^R + r.  In place.
+//
+// Same field operations as the reference network, so the canonical outputs are bit-identical.
+// Per column: reads n + D n + D n, writes n (+ n monomials) + D n + D n words, against 4 n + 4 D n
+// in the two-pass form.
+#include <hip/hip_runtime.h>
+#include "gl.hpp"
+#include "gl_asm.hpp"
+#include "ntt_pow2.hpp"
+#include "ntt_ct_common.hpp"
+#include "bj_internal.hpp"
+
+namespace bj {
+
+namespace {
+
+// table of one coset shift s (launch_lde3_table), for log n = R + 13:
+//   [0, 8192)            CT13[2^u + g] = s^(n >> (u+1)) w_{2^(u+1)}^bitrev_u(g), u < 13 (forward phase C)
+//   [L3_HA, +32)         s^((n/32) k)                                  (forward phase A)
+//   [L3_HB, +1024)       sigma_5(g)^((n/1024) k) at 32 g + k            (forward phase B)
+//   [L3_F1, +2^18)       sigma_13(M)^(2^(R-5) k) at k 8192 + M          (final phase 1)
+//   [L3_U, +2^R)         w_{2^R}^(bitrev_5(p) rl) at p 2^(R-5) + rl     (final phase 2, universal)
+//   [L3_A, +n/32)        sigma_13(M)^rl at rl 8192 + M                  (final phase 2)
+//   [L3_F2, +n) (R > 5)  sigma_18(32 M + p)^rl at (32 rl + p) 8192 + M  (final phase 2, tabulated)
+// with sigma_u(g) = s w_n^bitrev_u(g), the coset of group g after u stages.  Phase 2's factor
+// sigma_18(32 M + p)^rl = A[rl][M] U[p][rl], since sigma_18(32 M + p) = sigma_13(M) w_{2^R}^bitrev_5(p).
+// F1, A and F2 are laid out M-fastest, so the W lanes of a final block that share a row read
+// consecutive words.
+constexpr size_t L3_HA = 8192;
+constexpr size_t L3_HB = L3_HA + 32;
+constexpr size_t L3_F1 = L3_HB + 1024;
+constexpr size_t L3_U = L3_F1 + ((size_t)1 << 18);
+constexpr size_t L3_A = L3_U + 1024;
+constexpr size_t L3_F2 = L3_A + ((size_t)1 << 18);
+
+__host__ __device__ constexpr uint32_t cbrev(uint32_t x, int bits) {
+    uint32_t r = 0;
+    for (int i = 0; i < bits; i++) r |= ((x >> i) & 1u) << (bits - 1 - i);
+    return r;
+}
+
+__device__ __forceinline__ uint32_t brev(uint32_t x, int bits) {
+    return bits == 0 ? 0u : (__builtin_bitreverse32(x) >> (32 - bits));
+}
+
+// y[k] = x[bitrev_5(k)] * f[k]: a prescale whose inputs sit in bit-reversed register order
+// (general products, any u64 representative)
+__device__ __forceinline__ void prescale32_brev(uint64_t* y, const uint64_t* x, const uint64_t* f) {
+#pragma unroll
+    for (int k = 0; k < PT; k += 4) {
+        uint32_t z0[4], z1[4];
+        const uint64_t a0 = x[cbrev(k, 5)], a1 = x[cbrev(k + 1, 5)], a2 = x[cbrev(k + 2, 5)], a3 = x[cbrev(k + 3, 5)];
+        glasm::mul_x4((uint32_t)a0, (uint32_t)(a0 >> 32), (uint32_t)f[k], (uint32_t)(f[k] >> 32), z0[0], z1[0],
+                      (uint32_t)a1, (uint32_t)(a1 >> 32), (uint32_t)f[k + 1], (uint32_t)(f[k + 1] >> 32), z0[1], z1[1],
+                      (uint32_t)a2, (uint32_t)(a2 >> 32), (uint32_t)f[k + 2], (uint32_t)(f[k + 2] >> 32), z0[2], z1[2],
+                      (uint32_t)a3, (uint32_t)(a3 >> 32), (uint32_t)f[k + 3], (uint32_t)(f[k + 3] >> 32), z0[3],
+                      z1[3]);
+#pragma unroll
+        for (int i = 0; i < 4; i++) y[k + i] = join2(z0[i], z1[i]);
+    }
+}
+
+// A raw buffer descriptor whose base is provably wave-uniform (readfirstlane on both halves:
+// otherwise every buffer access through it becomes a waterfall loop)
+__device__ __forceinline__ __amdgpu_buffer_rsrc_t uniform_rsrc(const uint64_t* p, uint32_t bytes) {
+    const uint64_t a = (uint64_t)p;
+    const uint32_t lo = __builtin_amdgcn_readfirstlane((uint32_t)a);
+    const uint32_t hi = __builtin_amdgcn_readfirstlane((uint32_t)(a >> 32));
+    return __builtin_amdgcn_make_buffer_rsrc((void*)(((uint64_t)hi << 32) | lo), 0, (int)bytes, 0x00020000);
+}
+
+typedef unsigned int u32x2 __attribute__((ext_vector_type(2)));
+__device__ __forceinline__ u32x2 as_u32x2(uint64_t v) {
+    u32x2 r;
+    r.x = (uint32_t)v;
+    r.y = (uint32_t)(v >> 32);
+    return r;
+}
+
+// x[k] *= f[k] for k < 16
+__device__ __forceinline__ void prescale16(uint64_t* x, const uint64_t* f) {
+#pragma unroll
+    for (int k = 0; k < 16; k += 4) {
+        uint32_t z0[4], z1[4];
+        glasm::mul_x4((uint32_t)x[k], (uint32_t)(x[k] >> 32), (uint32_t)f[k], (uint32_t)(f[k] >> 32), z0[0], z1[0],
+                      (uint32_t)x[k + 1], (uint32_t)(x[k + 1] >> 32), (uint32_t)f[k + 1], (uint32_t)(f[k + 1] >> 32),
+                      z0[1], z1[1], (uint32_t)x[k + 2], (uint32_t)(x[k + 2] >> 32), (uint32_t)f[k + 2],
+                      (uint32_t)(f[k + 2] >> 32), z0[2], z1[2], (uint32_t)x[k + 3], (uint32_t)(x[k + 3] >> 32),
+                      (uint32_t)f[k + 3], (uint32_t)(f[k + 3] >> 32), z0[3], z1[3]);
+#pragma unroll
+        for (int i = 0; i < 4; i++) x[k + i] = join2(z0[i], z1[i]);
+    }
+}
+
+// y[k] = x[bitrev_5(k)] * h[k] with h wave-uniform (the phase-A factors s^((n/32) k), one table per
+// coset): the factors stay in SGPRs (scalar loads, mul_sb_x4), so they take no VGPRs next to the
+// monomials, the phase's values and its output
+__device__ __forceinline__ void prescale32_brev_uniform(uint64_t* y, const uint64_t* x, const uint64_t* __restrict__ h) {
+#pragma unroll
+    for (int k = 0; k < PT; k += 4) {
+        uint32_t z0[4], z1[4];
+        const uint64_t a0 = x[cbrev(k, 5)], a1 = x[cbrev(k + 1, 5)], a2 = x[cbrev(k + 2, 5)], a3 = x[cbrev(k + 3, 5)];
+        const uint64_t f0 = h[k], f1 = h[k + 1], f2 = h[k + 2], f3 = h[k + 3];
+        glasm::mul_sb_x4((uint32_t)a0, (uint32_t)(a0 >> 32), (uint32_t)f0, (uint32_t)(f0 >> 32), z0[0], z1[0],
+                         (uint32_t)a1, (uint32_t)(a1 >> 32), (uint32_t)f1, (uint32_t)(f1 >> 32), z0[1], z1[1],
+                         (uint32_t)a2, (uint32_t)(a2 >> 32), (uint32_t)f2, (uint32_t)(f2 >> 32), z0[2], z1[2],
+                         (uint32_t)a3, (uint32_t)(a3 >> 32), (uint32_t)f3, (uint32_t)(f3 >> 32), z0[3], z1[3]);
+#pragma unroll
+        for (int i = 0; i < 4; i++) y[k + i] = join2(z0[i], z1[i]);
+    }
+}
+
+// ------------------------------------------------------------------ middle pass
+//
+// LDS layouts of the forward exchanges (element m = position within the block after the
+// forward stages, j = m 2^R + r; l = bitrev_13(m)), each bank-conflict free for its reads and
+// writes (checked on the host, tests/test_lde3_layout.py):
+//   phase A out, m = 256 k + bitrev_8(t)          l-padded: 33 t + bitrev_5(k)
+//   phase B, m = 256 g + 8 k + b, g = bitrev_5(t & 31), b = bitrev_3(t >> 5)
+//                                                 l-padded: 1056 (t >> 5) + (t & 31) + 33 bitrev_5(k)
+//   phase C read, m = 32 t + k                    l-padded: s8 + (s8 >> 5) + 264 bitrev_5(k), s8 = bitrev_8(t)
+//   phase C out, m = 32 t + k                     m-padded: 33 t + k
+//   store, m = t + 256 k                          m-padded: t + (t >> 5) + 264 k
+template <int R, bool INV_PART, bool MONO>
+__global__ __launch_bounds__(NT, 2) void lde3_mid_kernel(const uint64_t* src, size_t src_stride, uint64_t* mono,
+                                                         size_t mono_stride, uint64_t* lde, size_t col_stride,
+                                                         size_t coset_stride, uint32_t n_cols, uint32_t n_cosets,
+                                                         const uint64_t* __restrict__ inv_tab,
+                                                         const uint64_t* __restrict__ tabs, size_t tab_stride) {
+    constexpr uint32_t LOGN = R + 13;
+    constexpr int LW = 13 - R;
+    constexpr uint32_t W = 1u << LW;
+    __shared__ uint64_t lds[PAD_LDS];
+    const uint32_t t = threadIdx.x;
+    // columns fastest: the blocks of one q (same inverse-table slices) run together
+    // (readfirstlane: the division runs on the VALU, and the block's bases belong in SGPRs)
+    const uint32_t c = __builtin_amdgcn_readfirstlane(blockIdx.x % n_cols);
+    const uint32_t q = __builtin_amdgcn_readfirstlane(blockIdx.x / n_cols);
+    const uint64_t* blk = src + (size_t)c * src_stride + (size_t)q * TILE;
+    const uint32_t ba = tail_base_a(t), bc = tail_base_c(t);
+    uint64_t x[PT];
+#pragma unroll
+    for (int k = 0; k < PT; k++) x[k] = blk[t + NT * k];
+    if constexpr (INV_PART) {
+        // the inverse tail (ct_tail_kernel<., true>): local stages 0..12 of block q, n^-1 in TA
+        const uint64_t* ext = inv_tab + ((size_t)1 << LOGN);
+        uint64_t f[PT], wa[16], wb[16], wc[16];
+        load32(f, ext + EXT_TA + (size_t)q * 32);
+        prescale32(x, f);
+        dft_p2<5, true, 0>(x);
+        const uint32_t tlo = t & 7, thi = t >> 3;
+        const uint32_t bb = tail_base_b(thi, tlo);
+#pragma unroll
+        for (int k = 0; k < PT; k++) lds[ba + tail_off_a(k)] = x[k];
+        load32(f, ext + ext_tb(R) + ((((size_t)q << 5) | thi) << 5));
+        __syncthreads();
+#pragma unroll
+        for (int k = 0; k < PT; k++) x[k] = lds[bb + tail_off_b(k)];
+        prescale32(x, f);
+        dft_p2<5, true, 0>(x);
+        tw_ct_tailC<10>(wa, inv_tab, R, q, t);
+        // same slots as the reads just made by this thread: no barrier needed before the writes
+#pragma unroll
+        for (int k = 0; k < PT; k++) lds[bb + tail_off_b(k)] = x[k];
+        tw_ct_tailC<11>(wb, inv_tab, R, q, t);
+        tw_ct_tailC<12>(wc, inv_tab, R, q, t);
+        __syncthreads();
+#pragma unroll
+        for (int k = 0; k < PT; k++) x[k] = lds[bc + k];
+        ct_stage<4>(x, wa);
+        ct_stage<2>(x, wb);
+        ct_stage<1>(x, wc);
+    } else {
+        // monomials already in bit-reversed order: re-deal the coalesced load to l = 32 t + k
+#pragma unroll
+        for (int k = 0; k < PT; k++) lds[ba + tail_off_a(k)] = x[k];
+        __syncthreads();
+#pragma unroll
+        for (int k = 0; k < PT; k++) x[k] = lds[bc + k];
+    }
+    // x[k] = c_j at block position l = 32 t + k: j = bitrev_13(l) 2^R + bitrev_R(q)
+    if constexpr (MONO) {
+        // the canonical monomials back to the block (bj_lde_d's scratch contract), coalesced
+        // through the tail's epilogue exchange (l-padded C writes, A reads)
+#pragma unroll
+        for (int k = 0; k < PT; k += 4) {
+            uint64_t v[4] = {x[k], x[k + 1], x[k + 2], x[k + 3]};
+            canon4(v);
+#pragma unroll
+            for (int i = 0; i < 4; i++) lds[bc + k + i] = v[i];
+        }
+        __syncthreads();
+        uint64_t* mo = mono + (size_t)c * mono_stride + (size_t)q * TILE;
+#pragma unroll
+        for (int k = 0; k < PT; k++) mo[t + NT * k] = lds[ba + tail_off_a(k)];
+    }
+    const uint32_t s8 = brev(t, 8);
+    const uint32_t b1 = 33 * t;                                  // phase A out (l-padded)
+    const uint32_t b2 = 1056 * (t >> 5) + (t & 31);              // phase B (l-padded)
+    const uint32_t b3 = s8 + (s8 >> 5);                          // phase C read (l-padded)
+    const uint32_t g5 = brev(t & 31, 5);                         // phase-B group of this thread
+    // store: m = t + 256 k -> run T = (t >> LW) + k 2^(8-LW), word q W + (t & (W-1)) of it
+    const uint32_t vo = ((t >> LW) << 13) + q * W + (t & (W - 1));
+#pragma unroll 1
+    for (uint32_t i = 0; i < n_cosets; i++) {
+        const uint64_t* tab = tabs + (size_t)i * tab_stride;
+        uint64_t y[PT], f[PT];
+        // phase A (forward stages 0..4): register k holds m's top 5 bits bitrev_5(k)
+        prescale32_brev_uniform(y, x, tab + L3_HA);
+        dft_p2<5, false, 0>(y);
+        __syncthreads();  // the previous coset's (or the monomial epilogue's) LDS reads are done
+#pragma unroll
+        for (int k = 0; k < PT; k++) lds[b1 + cbrev(k, 5)] = y[k];
+        // phase B's first 16 factors ahead of the barrier, the other 16 after the first products
+        // (64 VGPRs of factors next to the monomials and the phase's values spill)
+        const uint64_t* hb = tab + L3_HB + 32 * g5;
+#pragma unroll
+        for (int k = 0; k < 16; k++) f[k] = hb[k];
+        __syncthreads();
+#pragma unroll
+        for (int k = 0; k < PT; k++) y[k] = lds[b2 + 33 * cbrev(k, 5)];
+        // phase B (stages 5..9): group g5, coefficient distance n / 1024
+        prescale16(y, f);
+#pragma unroll
+        for (int k = 16; k < PT; k++) f[k] = hb[k];
+        prescale16(y + 16, f + 16);
+        dft_p2<5, false, 0>(y);
+        uint64_t wa[16], wb[16], wc[16];
+        tw_ct_tailC<10>(wa, tab, 0, 0, t);
+#pragma unroll
+        for (int k = 0; k < PT; k++) lds[b2 + 33 * cbrev(k, 5)] = y[k];
+        tw_ct_tailC<11>(wb, tab, 0, 0, t);
+        tw_ct_tailC<12>(wc, tab, 0, 0, t);
+        __syncthreads();
+#pragma unroll
+        for (int k = 0; k < PT; k++) y[k] = lds[b3 + 264 * cbrev(k, 5)];
+        // phase C (stages 10..12), general twiddles CT13[2^u + (m >> (13 - u))]
+        ct_stage<4>(y, wa);
+        ct_stage<2>(y, wb);
+        ct_stage<1>(y, wc);
+        __syncthreads();
+#pragma unroll
+        for (int k = 0; k < PT; k++) lds[bc + k] = y[k];
+        __syncthreads();
+#pragma unroll
+        for (int k = 0; k < PT; k++) y[k] = lds[ba + tail_off_a(k)];
+        // buffer stores: the coset column's base in the descriptor (SGPRs), the per-thread word
+        // offset in voffset and each register's run offset k 2^(21 - LW) words in soffset (plain
+        // stores made a 64-bit VGPR address per register)
+        const auto rs = uniform_rsrc(lde + (size_t)c * col_stride + (size_t)i * coset_stride, 8u << LOGN);
+#pragma unroll
+        for (int k = 0; k < PT; k++)
+            __builtin_amdgcn_raw_buffer_store_b64(as_u32x2(y[k]), rs, (int)(vo * 8), (int)((uint32_t)k << (24 - LW)),
+                                                  0);
+    }
+}
+
+// ------------------------------------------------------------------- final pass
+//
+// Region T of a coset's column: element (q, o) at q W + o, M = T W + o, r = bitrev_R(q).
+// Phase 1 (stages 13..17, r's top 5 bits = q's low 5): thread (qh = t >> LW, o = t & (W-1)) holds
+// q = 32 qh + k.  Phase 2 (stages 18..12+R, r's low R-5 bits): thread (o, pl = t >> LW) holds
+// groups p = pl + 2^(R-5) h, register h 2^(R-5) + rl <-> r = 2^(R-5) p + rl.  Store: position
+// P = t + 256 k = o 2^R + r.  LDS layouts (conflict-free or nearly, tests/test_lde3_layout.py):
+// "r-order" slot(e) = e + (e >> 5), e = r W + o, for R >= 6; "P-order" e = o 2^R + r at R = 5.
+template <int R>
+__device__ __forceinline__ constexpr uint32_t fin_slot(uint32_t r, uint32_t o) {
+    const uint32_t e = R == 5 ? (o << R) + r : r * (1u << (13 - R)) + o;
+    return e + (e >> 5);
+}
+// (r, o) of the three access patterns for thread t, register k
+template <int R>
+__device__ __forceinline__ constexpr uint32_t fin_p1(uint32_t t, uint32_t k) {
+    constexpr int LW = 13 - R;
+    return fin_slot<R>((k << (R - 5)) + cbrev(t >> LW, R - 5), t & ((1u << LW) - 1));
+}
+template <int R>
+__device__ __forceinline__ constexpr uint32_t fin_p2(uint32_t t, uint32_t k) {
+    constexpr int LW = 13 - R;
+    const uint32_t h = k >> (R - 5), rl = k & ((1u << (R - 5)) - 1);
+    const uint32_t p = (t >> LW) + (h << (R - 5));
+    return fin_slot<R>((p << (R - 5)) + rl, t & ((1u << LW) - 1));
+}
+template <int R>
+__device__ __forceinline__ constexpr uint32_t fin_p3(uint32_t t, uint32_t k) {
+    const uint32_t P = t + 256 * k;
+    return fin_slot<R>(P & ((1u << R) - 1), P >> R);
+}
+
+// Phase factors: phase 1's sigma_13(M)^(2^(R-5) k) (F1) and phase 2's sigma_18(32 M + p)^rl.
+// * F1: 32 W distinct words per block, each used by 2^(R-5) threads: for R >= 8 the block stages
+//   its slice in LDS (W / 8 coalesced loads per thread instead of 32), else direct loads.
+// * phase 2: F2MODE 0 (production) loads the tabulated F2 (one distinct word per element, 64 KiB
+//   per block, shared by the columns in L2) at the kernel's start, so the loads overlap phase 1;
+//   F2MODE 1 forms A[rl][M] U[p][rl] from slices staged in LDS (256 + 32 2^(R-5) words per block)
+//   with one extra product per element.  C3 (tools/lde3_ablation.hip, profiles/r3d_lde3_ablation.log):
+//   17.4 ms against 18.5; both loading F1 and F2 directly at their use: 21.0.
+template <int R>
+struct FinLds {
+    static constexpr int LW = 13 - R, RL = R - 5;
+    static constexpr uint32_t W = 1u << LW;
+    static constexpr bool F1_LDS = R >= 8;
+    static constexpr uint32_t F1 = F1_LDS ? 32 * W : 0;      // [k][o]
+    static constexpr uint32_t A = (1u << RL) * W;             // [rl][o]
+    static constexpr uint32_t UP = (1u << RL) + 1;            // padded row of U: [p][rl], p rows of UP
+    static constexpr uint32_t U = 32 * UP;
+};
+
+template <int R, int F2MODE>
+__global__ __launch_bounds__(NT, 2) void lde3_final_kernel(uint64_t* lde, size_t col_stride, size_t coset_stride,
+                                                           uint32_t n_cols, uint32_t n_cosets,
+                                                           const uint64_t* __restrict__ tabs, size_t tab_stride) {
+    using FL = FinLds<R>;
+    constexpr int LW = FL::LW, RL = FL::RL;
+    constexpr uint32_t W = FL::W;
+    __shared__ uint64_t lds[PAD_LDS];
+    __shared__ uint64_t lf1[FL::F1 ? FL::F1 : 1];
+    __shared__ uint64_t la[R > 5 && F2MODE == 1 ? FL::A : 1];
+    __shared__ uint64_t lu[R > 5 && F2MODE == 1 ? FL::U : 1];
+    const uint32_t t = threadIdx.x;
+    // columns fastest: the blocks of one (coset, region) share its table slices in L2
+    const uint32_t c = __builtin_amdgcn_readfirstlane(blockIdx.x % n_cols);
+    const uint32_t rest = blockIdx.x / n_cols;
+    const uint32_t i = __builtin_amdgcn_readfirstlane(rest % n_cosets);
+    const uint32_t T = __builtin_amdgcn_readfirstlane(rest / n_cosets);
+    uint64_t* d = lde + (size_t)c * col_stride + (size_t)i * coset_stride + (size_t)T * TILE;
+    const uint64_t* tab = tabs + (size_t)i * tab_stride;
+    const uint32_t o = t & (W - 1), qh = t >> LW;
+    const uint32_t M0 = T * W, M = M0 + o;
+    uint64_t x[PT], y[PT], f[PT];
+    const uint32_t vi = qh * 32 * W + o;
+#pragma unroll
+    for (int k = 0; k < PT; k++) x[k] = d[vi + k * W];
+    // table slices into LDS (coalesced: consecutive threads, consecutive M)
+    if constexpr (FL::F1_LDS) {
+#pragma unroll
+        for (uint32_t e = t; e < FL::F1; e += NT) lf1[e] = tab[L3_F1 + ((size_t)(e >> LW) << 13) + M0 + (e & (W - 1))];
+    }
+    if constexpr (R > 5 && F2MODE == 1) {
+        la[t] = tab[L3_A + ((size_t)(t >> LW) << 13) + M0 + (t & (W - 1))];
+#pragma unroll
+        for (uint32_t e = t; e < (32u << RL); e += NT) lu[(e >> RL) * FL::UP + (e & ((1u << RL) - 1))] = tab[L3_U + e];
+    }
+    uint64_t g2[F2MODE == 0 && R > 5 ? PT : 1];
+    if constexpr (F2MODE == 0 && R > 5) {
+        // tabulated phase-2 factors, issued early so their latency overlaps phase 1
+        const uint64_t* f2 = tab + L3_F2 + M + ((size_t)(t >> LW) << 13);
+#pragma unroll
+        for (int k = 0; k < PT; k++) {
+            const uint32_t h = k >> RL, rl = k & ((1u << RL) - 1);
+            g2[k] = f2[(size_t)(rl * 32 + (h << RL)) << 13];
+        }
+    }
+    if constexpr (FL::F1_LDS) {
+        __syncthreads();
+#pragma unroll
+        for (int k = 0; k < PT; k++) f[k] = lf1[k * W + o];
+    } else {
+        const uint64_t* f1 = tab + L3_F1 + M;
+#pragma unroll
+        for (int k = 0; k < PT; k++) f[k] = f1[(size_t)k << 13];
+    }
+    // phase 1: prescale sigma_13(M)^(2^(R-5) k), DFT over r's top 5 bits
+    prescale32_brev(y, x, f);
+    dft_p2<5, false, 0>(y);
+    const uint32_t b1 = fin_p1<R>(t, 0);
+#pragma unroll
+    for (int k = 0; k < PT; k++) lds[b1 + (fin_p1<R>(0, k) - fin_p1<R>(0, 0))] = y[k];
+    if constexpr (R > 5) {
+        // phase 2 factors for groups p = pl + 2^(R-5) h, register h 2^(R-5) + rl
+        const uint32_t pl = t >> LW;
+        if constexpr (F2MODE == 1) {
+            if constexpr (!FL::F1_LDS) __syncthreads();  // la / lu written
+            uint64_t a[PT];
+#pragma unroll
+            for (int k = 0; k < PT; k++) {
+                const uint32_t h = k >> RL, rl = k & ((1u << RL) - 1);
+                a[k] = la[rl * W + o];
+                f[k] = lu[(pl + (h << RL)) * FL::UP + rl];
+            }
+            prescale32(f, a);
+        } else {
+#pragma unroll
+            for (int k = 0; k < PT; k++) f[k] = g2[k];
+        }
+        __syncthreads();
+        const uint32_t b2 = fin_p2<R>(t, 0);
+#pragma unroll
+        for (int k = 0; k < PT; k++) y[k] = lds[b2 + (fin_p2<R>(0, k) - fin_p2<R>(0, 0))];
+        prescale32(y, f);
+        dft_p2_groups<RL, false>(y);
+        // same slots as this thread's reads: no barrier before the writes
+#pragma unroll
+        for (int k = 0; k < PT; k++) lds[b2 + (fin_p2<R>(0, k) - fin_p2<R>(0, 0))] = y[k];
+    }
+    __syncthreads();
+    const uint32_t b3 = fin_p3<R>(t, 0);
+#pragma unroll
+    for (int k = 0; k < PT; k++) y[k] = lds[b3 + (fin_p3<R>(0, k) - fin_p3<R>(0, 0))];
+#pragma unroll
+    for (int k = 0; k < PT; k += 4) canon4(y + k);
+#pragma unroll
+    for (int k = 0; k < PT; k++) d[t + NT * k] = y[k];
+}
+
+// ------------------------------------------------------------------- table
+__global__ void lde3_table_kernel(uint64_t* out, uint32_t log_n, uint64_t w_n, uint64_t s, size_t len) {
+    const size_t n = (size_t)1 << log_n;
+    const uint32_t R = log_n - 13;
+    for (size_t idx = blockIdx.x * (size_t)blockDim.x + threadIdx.x; idx < len;
+         idx += (size_t)gridDim.x * blockDim.x) {
+        uint64_t v;
+        if (idx < L3_HA) {
+            if (idx == 0) {
+                v = 0;
+            } else {
+                const uint32_t u = 31 - __builtin_clz((uint32_t)idx);
+                const uint32_t g = (uint32_t)idx - (1u << u);
+                const uint64_t e = (uint64_t)gl::bitrev32(g, u) << (log_n - u - 1);
+                v = gl::mul(gl::pow(w_n, e), gl::pow(s, n >> (u + 1)));
+            }
+        } else if (idx < L3_HB) {
+            v = gl::pow(s, (n >> 5) * (idx - L3_HA));
+        } else if (idx < L3_F1) {
+            const uint32_t j = (uint32_t)(idx - L3_HB);
+            const uint64_t sigma = gl::mul(s, gl::pow(w_n, gl::bitrev32(j >> 5, 5)));
+            v = gl::pow(sigma, (n >> 10) * (j & 31));
+        } else if (idx < L3_U) {
+            const uint32_t j = (uint32_t)(idx - L3_F1);
+            const uint32_t M = j & 8191, k = j >> 13;
+            const uint64_t sigma = gl::mul(s, gl::pow(w_n, gl::bitrev32(M, 13)));
+            v = gl::pow(sigma, (uint64_t)k << (R - 5));
+        } else if (idx < L3_A) {
+            // w_{2^R} = w_n^(2^13)
+            const uint32_t j = (uint32_t)(idx - L3_U);
+            const uint32_t p = j >> (R - 5), rl = j & ((1u << (R - 5)) - 1);
+            v = (j >> R) ? 0 : gl::pow(gl::pow(w_n, 8192), (uint64_t)gl::bitrev32(p, 5) * rl);
+        } else if (idx < L3_F2) {
+            const uint32_t j = (uint32_t)(idx - L3_A);
+            const uint32_t M = j & 8191, rl = j >> 13;
+            const uint64_t sigma = gl::mul(s, gl::pow(w_n, gl::bitrev32(M, 13)));
+            v = (rl >> (R - 5)) ? 0 : gl::pow(sigma, rl);
+        } else {
+            const size_t j = idx - L3_F2;
+            const uint32_t M = (uint32_t)(j & 8191), rest = (uint32_t)(j >> 13);
+            const uint32_t p = rest & 31, rl = rest >> 5;
+            const uint64_t sigma = gl::mul(s, gl::pow(w_n, gl::bitrev32(M * 32 + p, 18)));
+            v = gl::pow(sigma, rl);
+        }
+        out[idx] = gl::canon(v);
+    }
+}
+
+template <int R>
+void launch_lde3_R(uint64_t* lde, size_t col_stride, size_t coset_stride, uint32_t n_cosets, const uint64_t* src,
+                   size_t src_stride, uint64_t* mono, size_t mono_stride, uint32_t n_cols, const uint64_t* inv_tab,
+                   const uint64_t* tabs, size_t tab_stride, hipStream_t st) {
+    const dim3 gm(n_cols << R);
+    if (inv_tab && mono)
+        hipLaunchKernelGGL((lde3_mid_kernel<R, true, true>), gm, dim3(NT), 0, st, src, src_stride, mono, mono_stride,
+                           lde, col_stride, coset_stride, n_cols, n_cosets, inv_tab, tabs, tab_stride);
+    else if (inv_tab)
+        hipLaunchKernelGGL((lde3_mid_kernel<R, true, false>), gm, dim3(NT), 0, st, src, src_stride, mono,
+                           mono_stride, lde, col_stride, coset_stride, n_cols, n_cosets, inv_tab, tabs, tab_stride);
+    else
+        hipLaunchKernelGGL((lde3_mid_kernel<R, false, false>), gm, dim3(NT), 0, st, src, src_stride, mono,
+                           mono_stride, lde, col_stride, coset_stride, n_cols, n_cosets, inv_tab, tabs, tab_stride);
+    const dim3 gf((n_cols * n_cosets) << R);
+    hipLaunchKernelGGL((lde3_final_kernel<R, 0>), gf, dim3(NT), 0, st, lde, col_stride, coset_stride, n_cols,
+                       n_cosets, tabs, tab_stride);
+}
+
+}  // namespace
+
+bool lde3_supported(uint32_t log_n) { return log_n >= 18 && log_n <= 23; }
+
+size_t lde3_table_len(uint32_t log_n) {
+    return log_n > 18 ? L3_F2 + ((size_t)1 << log_n) : L3_F2;
+}
+
+hipError_t launch_lde3_table(uint64_t* out, uint32_t log_n, uint64_t shift, hipStream_t st) {
+    if (!lde3_supported(log_n)) return hipErrorInvalidValue;
+    const size_t len = lde3_table_len(log_n);
+    size_t blocks = (len + 255) / 256;
+    if (blocks > 16384) blocks = 16384;
+    hipLaunchKernelGGL(lde3_table_kernel, dim3((unsigned)blocks), dim3(256), 0, st, out, log_n,
+                       gl::domain_generator(log_n), gl::canon(shift), len);
+    return hipGetLastError();
+}
+
+hipError_t launch_lde3(uint64_t* lde, size_t col_stride, size_t coset_stride, uint32_t n_cosets, const uint64_t* src,
+                       size_t src_stride, uint64_t* mono, size_t mono_stride, uint32_t n_cols, uint32_t log_n,
+                       const uint64_t* inv_tab, const uint64_t* tabs, size_t tab_stride, hipStream_t st) {
+    if (n_cols == 0 || n_cosets == 0) return hipSuccess;
+    if (!lde3_supported(log_n)) return hipErrorInvalidValue;
+    if (((uint64_t)n_cols * n_cosets) << (log_n - 13) > 0x7fffffffull) return hipErrorInvalidValue;
+#define BJ_LDE3(RR)                                                                                              \
+    launch_lde3_R<RR>(lde, col_stride, coset_stride, n_cosets, src, src_stride, mono, mono_stride, n_cols, inv_tab, \
+                      tabs, tab_stride, st)
+    switch (log_n - 13) {
+        case 5: BJ_LDE3(5); break;
+        case 6: BJ_LDE3(6); break;
+        case 7: BJ_LDE3(7); break;
+        case 8: BJ_LDE3(8); break;
+        case 9: BJ_LDE3(9); break;
+        default: BJ_LDE3(10); break;
+    }
+#undef BJ_LDE3
+    return hipGetLastError();
+}
+
+}  // namespace bj

@@ -242,7 +242,7 @@ def pad(merged):
     return out
 
 
-def emit_fn(name, n, stream_fn, vper, in_names, out_names, in_kinds=None, doc="", out_kinds=None):
+def emit_fn(name, n, stream_fn, vper, in_names, out_names, in_kinds=None, doc="", out_kinds=None, in_cons=None):
     streams = [stream_fn(k, vper * k) for k in range(n)]
     body = interleave(streams)
     n_v = vper * n
@@ -254,7 +254,8 @@ def emit_fn(name, n, stream_fn, vper, in_names, out_names, in_kinds=None, doc=""
         for nm in out_names:
             args.append("%s& %s%d" % ((out_kinds or {}).get(nm, "uint32_t"), nm, k))
     outs = ", ".join('[%s%d] "=&v"(%s%d)' % (nm, k, nm, k) for k in range(n) for nm in out_names)
-    ins = ", ".join('[%s%d] "v"(%s%d)' % (nm, k, nm, k) for k in range(n) for nm in in_names)
+    ins = ", ".join('[%s%d] "%s"(%s%d)' % (nm, k, (in_cons or {}).get(nm, "v"), nm, k) for k in range(n)
+                    for nm in in_names)
     clob = ['"v%d"' % i for i in range(n_v)] + ['"s%d"' % i for i in range(SGPR_BASE, SGPR_BASE + 26)]
     lines = []
     if doc:
@@ -410,6 +411,53 @@ def emit_mi_layer_b():
     return "\n".join(lines) + "\n"
 
 
+SGPR_OPERANDS = True  # carry / constant SGPRs as compiler-allocated operands (False: fixed s40..)
+
+
+def sgpr_operandize(fn_text):
+    """Turn the fixed SGPRs of one generated asm function into compiler-allocated early-clobber
+    outputs: every pair s[a:a+1] becomes a uint64_t "=&s" operand %[qa] and every single sN a
+    uint32_t one %[kN]; their clobbers go.  The instruction order (and so the s_nop padding, which
+    depends only on the distances between an SGPR's writer and its readers) is unchanged, and
+    distinct operands get distinct registers, so the sequence computes the same values; what
+    changes is that the compiler is no longer barred from s40..s66 around every asm block (with
+    27 SGPRs clobbered, kernels that also need wave-uniform pointers ran short and kept them in
+    VGPRs).  The VGPR scratch stays fixed: pairs whose halves are also used alone cannot be
+    compiler operands (inline asm has no sub-register syntax)."""
+    if not SGPR_OPERANDS:
+        return fn_text
+    import re
+    lines = fn_text.split("\n")
+    try:
+        a = next(i for i, l in enumerate(lines) if l.strip() == "asm volatile(")
+    except StopIteration:
+        return fn_text
+    b = next(i for i in range(a, len(lines)) if lines[i].strip().startswith(": ") or lines[i].strip() == ":")
+    body = "\n".join(lines[a + 1:b])
+    pairs = sorted({int(m.group(1)) for m in re.finditer(r"\bs\[(\d+):(\d+)\]", body)})
+    singles = sorted({int(m.group(1)) for m in re.finditer(r"(?<![\w\[:])s(\d+)\b", body)})
+    assert not any(x in pairs or x - 1 in pairs for x in singles), "single SGPR inside a pair"
+    body = re.sub(r"\bs\[(\d+):(\d+)\]", lambda m: "%%[q%s]" % m.group(1), body)
+    body = re.sub(r"(?<![\w\[:])s(\d+)\b", lambda m: "%%[k%s]" % m.group(1), body)
+    outs_line = lines[b]
+    extra = ['[q%d] "=&s"(q%d)' % (x, x) for x in pairs] + ['[k%d] "=&s"(k%d)' % (x, x) for x in singles]
+    if extra:
+        if outs_line.strip() == ":":
+            outs_line = outs_line.rstrip() + " " + ", ".join(extra)
+        else:
+            outs_line = outs_line.rstrip() + ", " + ", ".join(extra)
+    clob_i = b + 2
+    clob = lines[clob_i]
+    clob = re.sub(r',?\s*"s\d+"', "", clob).replace(":,", ":").replace(": ,", ":")
+    decl = []
+    if pairs:
+        decl.append("    uint64_t %s;" % ", ".join("q%d" % x for x in pairs))
+    if singles:
+        decl.append("    uint32_t %s;" % ", ".join("k%d" % x for x in singles))
+    out = lines[:a] + decl + [lines[a]] + body.split("\n") + [outs_line, lines[b + 1], clob] + lines[clob_i + 1:]
+    return "\n".join(out)
+
+
 def main():
     parts = ['''// GENERATED by tools/gen_gl_asm.py -- do not edit.
 // gfx950 inline-asm Goldilocks primitives (see the generator's docstring for the
@@ -423,6 +471,11 @@ namespace glasm {
     for n in (1, 2, 3, 4):
         parts.append(emit_fn("mul_x%d" % n, n, mul_stream, 10, ["a0", "a1", "b0", "b1"], ["z0", "z1"],
                              doc="%d independent products z = a * b mod p (14 instructions each)" % n))
+    # the same products with a wave-uniform multiplier b in SGPRs (each mad reads one SGPR: gfx950's
+    # constant-bus limit), so uniform factors need no VGPR copies
+    parts.append(emit_fn("mul_sb_x4", 4, mul_stream, 10, ["a0", "a1", "b0", "b1"], ["z0", "z1"],
+                         in_cons={"b0": "s", "b1": "s"},
+                         doc="4 independent products z = a * b mod p, b wave-uniform in SGPRs (14 instructions each)"))
     for n in (1, 2, 3, 4):
         parts.append(emit_fn("reduce_x%d" % n, n, lambda k, vb: reduce_stream(k, vb, pair_out=True), 4,
                              ["L", "Hlo", "Hhi"], ["z"], in_kinds={"L": "uint64_t"}, out_kinds={"z": "uint64_t"},
@@ -441,6 +494,7 @@ namespace glasm {
     parts.append(emit_mi_layer_a())
     parts.append(emit_mi_layer_b())
     parts.append("}  // namespace glasm\n")
+    parts = [sgpr_operandize(x) for x in parts]
     with open(OUT, "w") as f:
         f.write("\n".join(parts))
     print("wrote", OUT)

@@ -26,7 +26,7 @@ import os
 import sys
 
 sys.path.insert(0, os.path.dirname(os.path.abspath(__file__)))
-from gen_gl_asm import BFLY_SCONST, JUNK, NEG_EPS_S, NEG_EPS_V, SGPR_BASE, merge, pad, sp  # noqa: E402
+from gen_gl_asm import BFLY_SCONST, JUNK, NEG_EPS_S, NEG_EPS_V, SGPR_BASE, merge, pad, sgpr_operandize, sp  # noqa: E402,E501
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 OUT = os.path.join(ROOT, "era-boojum_amd", "csrc", "ntt_pow2.hpp")
@@ -209,6 +209,7 @@ namespace glasm {
         for log_n in range(1, 6):
             parts.append(emit_dft(log_n, inverse))
     parts.append("#undef LO\n#undef HI\n}  // namespace p2dft\n}  // namespace bj\n")
+    parts = [sgpr_operandize(x) for x in parts]
     with open(OUT, "w") as f:
         f.write("\n".join(parts))
     print("wrote", OUT)
