@@ -10,7 +10,7 @@ cd "$GRAFT_REPO_ROOT"
 export TMPDIR=/tmp
 OUT=gpurun_out/prof_$TAG
 mkdir -p $OUT
-timeout -k 10 400 python3 bench.py > $OUT/bench_default.log 2>&1 || { echo "bench rc=$?"; tail -5 $OUT/bench_default.log; exit 1; }
+timeout -k 10 500 python3 bench.py > $OUT/bench_default.log 2>&1 || { echo "bench rc=$?"; tail -5 $OUT/bench_default.log; exit 1; }
 tail -1 $OUT/bench_default.log
 B="python3 bench.py --config C3 --no-cpu-baseline --no-native-base"
 timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d $OUT/trace -o run -- $B --steps 3 --warmup 1 > $OUT/trace.log 2>&1 || { echo "trace rc=$?"; tail -5 $OUT/trace.log; exit 1; }
@@ -24,7 +24,7 @@ echo sq ok
 timeout -s KILL 60 rocprofv3 --pmc FETCH_SIZE --output-format csv -d $OUT/cal_fetch -o run -- ./tools/fetch_calibration > $OUT/cal_fetch.log 2>&1 || { echo "cal fetch rc=$?"; tail -5 $OUT/cal_fetch.log; exit 1; }
 timeout -s KILL 60 rocprofv3 --pmc WRITE_SIZE --output-format csv -d $OUT/cal_write -o run -- ./tools/fetch_calibration > $OUT/cal_write.log 2>&1 || { echo "cal write rc=$?"; tail -5 $OUT/cal_write.log; exit 1; }
 echo calibration ok
-timeout -k 10 300 python3 tools/shard_compute_probe.py > $OUT/shard_compute.log 2>&1 || { echo "probe rc=$?"; tail -5 $OUT/shard_compute.log; exit 1; }
+PROBE_INTERFERE=1 timeout -k 10 400 python3 tools/shard_compute_probe.py > $OUT/shard_compute.log 2>&1 || { echo "probe rc=$?"; tail -5 $OUT/shard_compute.log; exit 1; }
 tail -1 $OUT/shard_compute.log
 if [ -x tools/pow2_bench ] && [ -x tools/bfly_bench ]; then
   timeout -k 10 120 ./tools/bfly_bench > $OUT/bfly_bench.log 2>&1 || { echo "bfly rc=$?"; exit 1; }

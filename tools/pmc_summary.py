@@ -33,6 +33,8 @@ KERNELS = [
     ("bj::(anonymous namespace)::ct_head_kernel<9, 1", "ct_head_fwd", 2.0),
     ("bj::(anonymous namespace)::ct_head_kernel<9, 0", "ct_head_inv", 2.0),
     ("bj::(anonymous namespace)::ct_tail_kernel", "ct_tail", 2.0),
+    ("bj::(anonymous namespace)::lde3_mid_kernel<9", "lde3_mid", 2.0),
+    ("bj::(anonymous namespace)::lde3_final_kernel<9", "lde3_final", 2.0),
     ("bj::(anonymous namespace)::dif_head_kernel<9, 1>", "dif_head_fwd", 2.0),
     ("bj::(anonymous namespace)::dif_head_kernel<9, 0>", "dif_head_inv", 2.0),
     ("bj::(anonymous namespace)::dif_tail_kernel", "dif_tail", 2.0),
@@ -96,10 +98,16 @@ def main():
             if c in d:
                 e[c.lower()] = d[c]
         out[k] = e
-    # the LDE phase as one unit: sum of its kernels per commit (one inverse head + tail, one
-    # forward head + tail; tail launches alternate inverse / forward)
+    # the LDE phase as one unit: sum of its kernels per commit.  Three-pass form: one inverse head,
+    # one middle and one final pass; two-pass form: one inverse head + tail, one forward head +
+    # tail (tail launches alternate inverse / forward)
+    l3 = [out.get(k) for k in ("ct_head_inv", "lde3_mid", "lde3_final")]
     ct = [out.get(k) for k in ("ct_head_inv", "ct_head_fwd", "ct_tail")]
-    if all(x and "hbm_bytes_per_launch" in x for x in ct):
+    if all(x and "hbm_bytes_per_launch" in x for x in l3):
+        out["lde"] = {"hbm_bytes_per_launch": sum(x["hbm_bytes_per_launch"] for x in l3),
+                      "note": "three-pass LDE: inverse head + middle + final, one commit",
+                      "src_hash": hashes.get("lde")}
+    elif all(x and "hbm_bytes_per_launch" in x for x in ct):
         out["lde"] = {"hbm_bytes_per_launch": ct[0]["hbm_bytes_per_launch"] + ct[1]["hbm_bytes_per_launch"]
                       + 2 * ct[2]["hbm_bytes_per_launch"], "note": "iNTT + forward, one commit",
                       "src_hash": hashes.get("lde")}

@@ -13,9 +13,91 @@ import json
 import os
 import sys
 
+# PROBE_INTERFERE=1: also the same calls beside an exchange-shaped disturbance (interference())
+
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, os.path.join(ROOT, "era-boojum_amd"))
 sys.path.insert(0, ROOT)
+
+
+# per-rank xGMI ingress of the exchange at G ranks: the links toward the other ranks (one per
+# peer on the 8-GPU node's full mesh, at most 7) at an effective per-link, per-direction rate
+LINK_GBS = (64.0, 153.0)
+
+
+def links(world):
+    return min(world - 1, 7)
+
+
+def _timed(comm, tr, res, n_cols, log_n, log_lde, cap, reps, disturb=None):
+    """ms per call on the compute stream and the phase split, optionally with `disturb(stream)`
+    launched on a high-priority side stream before each call (both streams joined after it)."""
+    import torch
+    from boojum_amd.sharded import native_sharded_commit
+    side = torch.cuda.Stream(priority=-1)
+    main = torch.cuda.current_stream()
+    comm.phase_ms()
+    comm.set_timing(True)
+    tot = 0.0
+    for _ in range(reps):
+        s, e = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        if disturb:
+            side.wait_stream(main)
+            disturb(side)
+        s.record()
+        native_sharded_commit(comm, tr, n_cols, log_n, log_lde, cap, out=res)
+        e.record()
+        if disturb:
+            main.wait_stream(side)
+        torch.cuda.synchronize()
+        tot += s.elapsed_time(e)
+    ph, calls = comm.phase_ms()
+    comm.set_timing(False)
+    return tot / reps, {k: v / max(1, calls) for k, v in ph.items()}
+
+
+def interference(comm, tr, res, n_cols, log_n, log_lde, cap, world, recv, reps, ph0, calls0):
+    """The same call beside a disturbance moving the `recv` bytes this rank receives per call
+    (what the exchange writes into its HBM), in three shapes:
+    * burst: torch copies on a high-priority stream, at full HBM speed (the round-2 probe: an
+      upper bound on memory contention, no CU residency like RCCL's);
+    * rccl-shaped: tools/paced_copy.hip, `channels` workgroups resident for the whole exchange
+      (as RCCL's collective kernels are) moving the bytes at the rank's xGMI ingress rate,
+      links(G) x LINK_GBS, for channels in 8 / 16 / 32.
+    Per shape: ms per call and the per-phase deltas (inverse + fold, LDE, leaves, nodes)."""
+    import ctypes
+    import torch
+    lib = ctypes.CDLL(os.path.join(ROOT, "tools", "libpaced_copy.so"))
+    lib.paced_copy.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_size_t, ctypes.c_size_t, ctypes.c_int,
+                               ctypes.c_double, ctypes.c_void_p]
+    ring = 512 << 20  # a 512 MiB ring: past the 256 MiB Infinity Cache, so the bytes reach HBM
+    a_buf = torch.empty(ring // 8, dtype=torch.int64, device="cuda")
+    b_buf = torch.empty_like(a_buf)
+    base_ms, base_ph = _timed(comm, tr, res, n_cols, log_n, log_lde, cap, reps)
+    rows = {"none": {"ms": round(base_ms, 2), "phase_ms": {k: round(v, 2) for k, v in base_ph.items()}}}
+
+    def burst(st):
+        with torch.cuda.stream(st):
+            for _ in range(max(1, recv // ring)):
+                b_buf.copy_(a_buf)
+
+    def paced(channels, gbps):
+        def f(st):
+            rc = lib.paced_copy(a_buf.data_ptr(), b_buf.data_ptr(), ring, recv, channels, gbps, st.cuda_stream)
+            if rc:
+                raise RuntimeError("paced_copy: hip error %d" % rc)
+        return f
+
+    shapes = [("burst", burst)]
+    for per_link in LINK_GBS:
+        for ch in (8, 16, 32):
+            shapes.append(("paced_%dch_%dGBs" % (ch, links(world) * per_link), paced(ch, links(world) * per_link)))
+    for name, fn in shapes:
+        ms, ph = _timed(comm, tr, res, n_cols, log_n, log_lde, cap, reps, fn)
+        rows[name] = {"ms": round(ms, 2), "delta_ms": round(ms - base_ms, 2),
+                      "phase_delta_ms": {k: round(ph[k] - base_ph[k], 2) for k in ph}}
+    del a_buf, b_buf
+    return rows
 
 
 def main():
@@ -58,29 +140,9 @@ def main():
             else 8 * n * n_cols * (world - 1) // world)
         interfered = None
         if recv and os.environ.get("PROBE_INTERFERE"):
-            # the same calls while a second, high-priority stream copies `recv` bytes device to
-            # device per call (what RCCL writes into this GPU's memory), to price the exchange's
-            # contention for CUs and HBM when it overlaps the compute
-            chunk = 256 << 20
-            a_buf = torch.empty(chunk // 8, dtype=torch.int64, device="cuda")
-            b_buf = torch.empty_like(a_buf)
-            side = torch.cuda.Stream(priority=-1)
-            s2, e2 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-            torch.cuda.synchronize()
-            s2.record()
-            for _ in range(reps):
-                side.wait_stream(torch.cuda.current_stream())
-                with torch.cuda.stream(side):
-                    for _ in range(max(1, recv // chunk)):
-                        b_buf.copy_(a_buf)
-                native_sharded_commit(comm, tr, n_cols, log_n, log_lde, cap, out=res)
-                torch.cuda.current_stream().wait_stream(side)
-            e2.record()
-            torch.cuda.synchronize()
-            interfered = round(s2.elapsed_time(e2) / reps, 2)
-            del a_buf, b_buf
+            interfered = interference(comm, tr, res, n_cols, log_n, log_lde, cap, world, recv, reps, ph, calls)
         out["%s_G%d" % (cfg, world)] = {
-            "ms_with_concurrent_copy_of_received_bytes": interfered,
+            "interference": interfered,
             "ms_per_rank": round(ms, 2), "ideal_elems_per_s": n_cols * n / (ms * 1e-3),
             "phase_ms": {k: round(v / max(1, calls), 2) for k, v in ph.items()},
             "exchange": "none" if world == 1 else ("all-to-all (sender fold)" if world > (1 << log_lde)

@@ -131,6 +131,28 @@ def ntt_census():
     return out
 
 
+def lde3_census():
+    """Per-wave issue slots of the three-pass LDE's kernels (ntt_lde3.hip) for R = log n - 13:
+    the middle pass lde3_mid_kernel<R, true, true> (the inverse tail + monomial store outside its
+    coset loop, one forward stage 0..12 set per loop trip) and the final pass
+    lde3_final_kernel<R, 0> (no loops).  bench.py prices the LDE phase with them (plus the
+    inverse head, head_inv above)."""
+    dis = disassemble("ntt_lde3")
+    out = {}
+    for r in range(5, 11):
+        ins = parse(kernel_lines(dis, "lde3_mid_kernelILi%dELb1ELb1E" % r))
+        if ins:
+            o, body = loop_census(ins)
+            out.setdefault("mid", {})[str(r)] = {"slots_outside_loop": o, "slots_per_coset": body}
+        ins = parse(kernel_lines(dis, "lde3_final_kernelILi%dELi0E" % r))
+        if ins:
+            v, s = straight_line(ins)
+            out.setdefault("final", {})[str(r)] = {"valu": v, "slots": s}
+    out["waves_per_block"] = 4
+    out["elements_per_block"] = 8192
+    return out
+
+
 def loop_census(instrs):
     """(slots outside the single loop, slots of one loop iteration) of a kernel with one loop."""
     base = instrs[0][0]
@@ -175,6 +197,7 @@ def main():
            "valu_instr_per_perm": valu, "issue_slots_per_perm": slots,
            "top": dict(sorted(hist.items(), key=lambda kv: -kv[1])[:12]),
            "ntt_ct": ntt_census(),
+           "lde3": lde3_census(),
            "blake2s": blake2s_census()}
     print(json.dumps(res, indent=1))
     if args.json:
