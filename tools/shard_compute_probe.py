@@ -29,26 +29,20 @@ def links(world):
     return min(world - 1, 7)
 
 
-def _timed(comm, tr, res, n_cols, log_n, log_lde, cap, reps, disturb=None):
-    """ms per call on the compute stream and the phase split, optionally with `disturb(stream)`
-    launched on a high-priority side stream before each call (both streams joined after it)."""
+def _timed(comm, tr, res, n_cols, log_n, log_lde, cap, reps):
+    """ms per call (events around it on the compute stream) and the phase split."""
     import torch
     from boojum_amd.sharded import native_sharded_commit
-    side = torch.cuda.Stream(priority=-1)
-    main = torch.cuda.current_stream()
+    native_sharded_commit(comm, tr, n_cols, log_n, log_lde, cap, out=res)  # warm-up
+    torch.cuda.synchronize()
     comm.phase_ms()
     comm.set_timing(True)
     tot = 0.0
     for _ in range(reps):
         s, e = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-        if disturb:
-            side.wait_stream(main)
-            disturb(side)
         s.record()
         native_sharded_commit(comm, tr, n_cols, log_n, log_lde, cap, out=res)
         e.record()
-        if disturb:
-            main.wait_stream(side)
         torch.cuda.synchronize()
         tot += s.elapsed_time(e)
     ph, calls = comm.phase_ms()
@@ -56,46 +50,46 @@ def _timed(comm, tr, res, n_cols, log_n, log_lde, cap, reps, disturb=None):
     return tot / reps, {k: v / max(1, calls) for k, v in ph.items()}
 
 
-def interference(comm, tr, res, n_cols, log_n, log_lde, cap, world, recv, reps, ph0, calls0):
-    """The same call beside a disturbance moving the `recv` bytes this rank receives per call
-    (what the exchange writes into its HBM), in three shapes:
-    * burst: torch copies on a high-priority stream, at full HBM speed (the round-2 probe: an
-      upper bound on memory contention, no CU residency like RCCL's);
-    * rccl-shaped: tools/paced_copy.hip, `channels` workgroups resident for the whole exchange
-      (as RCCL's collective kernels are) moving the bytes at the rank's xGMI ingress rate,
-      links(G) x LINK_GBS, for channels in 8 / 16 / 32.
-    Per shape: ms per call and the per-phase deltas (inverse + fold, LDE, leaves, nodes)."""
+def interference(comm0, tr, res, n_cols, log_n, log_lde, cap, world, recv, reps, ph0, calls0):
+    """The same call with each exchange replaced by an RCCL-shaped stand-in: a device-mode callback
+    transport (bj_comm_init_callback) whose exchange launches tools/paced_copy.hip on the stream
+    the library hands it -- the communicator's high-priority exchange stream, where RCCL's kernels
+    run -- moving the bytes this rank receives in that exchange, (G - 1) x the per-rank block, with
+    `channels` workgroups resident for the whole copy (as RCCL's collective kernels are) at the
+    rank's xGMI ingress rate, links(G) x LINK_GBS; "burst" is the same copy unpaced.  So the
+    compute stream sees the exchange's CU residency, its HBM traffic and its duration, chunk by
+    chunk, as the column pipeline issues them.  Per shape: ms per call, the delta against the
+    stubbed exchange, and the per-phase deltas (inverse + fold, LDE, leaves, nodes); the rest of a
+    delta is exchange the pipeline left exposed."""
     import ctypes
     import torch
+    from boojum_amd._lib import EXCHANGE_FN
+    from boojum_amd.sharded import NativeComm
     lib = ctypes.CDLL(os.path.join(ROOT, "tools", "libpaced_copy.so"))
     lib.paced_copy.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_size_t, ctypes.c_size_t, ctypes.c_int,
                                ctypes.c_double, ctypes.c_void_p]
     ring = 512 << 20  # a 512 MiB ring: past the 256 MiB Infinity Cache, so the bytes reach HBM
     a_buf = torch.empty(ring // 8, dtype=torch.int64, device="cuda")
     b_buf = torch.empty_like(a_buf)
-    base_ms, base_ph = _timed(comm, tr, res, n_cols, log_n, log_lde, cap, reps)
-    rows = {"none": {"ms": round(base_ms, 2), "phase_ms": {k: round(v, 2) for k, v in base_ph.items()}}}
-
-    def burst(st):
-        with torch.cuda.stream(st):
-            for _ in range(max(1, recv // ring)):
-                b_buf.copy_(a_buf)
-
-    def paced(channels, gbps):
-        def f(st):
-            rc = lib.paced_copy(a_buf.data_ptr(), b_buf.data_ptr(), ring, recv, channels, gbps, st.cuda_stream)
-            if rc:
-                raise RuntimeError("paced_copy: hip error %d" % rc)
-        return f
-
-    shapes = [("burst", burst)]
+    base_ms, base_ph = _timed(comm0, tr, res, n_cols, log_n, log_lde, cap, reps)
+    rows = {"stubbed": {"ms": round(base_ms, 2), "phase_ms": {k: round(v, 2) for k, v in base_ph.items()}}}
+    shapes = [("burst_32ch", 32, 0.0)]
     for per_link in LINK_GBS:
         for ch in (8, 16, 32):
-            shapes.append(("paced_%dch_%dGBs" % (ch, links(world) * per_link), paced(ch, links(world) * per_link)))
-    for name, fn in shapes:
-        ms, ph = _timed(comm, tr, res, n_cols, log_n, log_lde, cap, reps, fn)
+            shapes.append(("paced_%dch_%dGBs" % (ch, links(world) * per_link), ch, links(world) * per_link))
+    for name, ch, gbps in shapes:
+        def exchange(user, kind, send, recv_p, nbytes, stream, ch=ch, gbps=gbps):
+            moved = (world - 1) * nbytes
+            return lib.paced_copy(a_buf.data_ptr(), b_buf.data_ptr(), ring, max(moved, 1 << 18), ch, gbps, stream)
+        fn = EXCHANGE_FN(exchange)
+        comm = NativeComm._make("bj_comm_init_callback", world, 0, fn, None, 0, world=world, rank=0, keep=fn)
+        try:
+            ms, ph = _timed(comm, tr, res, n_cols, log_n, log_lde, cap, reps)
+        finally:
+            comm.close()
         rows[name] = {"ms": round(ms, 2), "delta_ms": round(ms - base_ms, 2),
-                      "phase_delta_ms": {k: round(ph[k] - base_ph[k], 2) for k in ph}}
+                      "phase_delta_ms": {k: round(ph[k] - base_ph[k], 2) for k in ph},
+                      "exposed_ms": round((ms - base_ms) - sum(ph[k] - base_ph[k] for k in ph), 2)}
     del a_buf, b_buf
     return rows
 
