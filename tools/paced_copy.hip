@@ -25,7 +25,15 @@ __global__ __launch_bounds__(256) void paced_copy_kernel(const uint4* __restrict
     uint64_t k = 0;
     for (size_t c = w; c * per < total16; c += G, k++) {
         const size_t base = (c * per) & (ring16 - 1);  // ring16: a power of two, a multiple of per
-        for (uint32_t i = threadIdx.x; i < per; i += blockDim.x) dst[base + i] = src[base + i];
+        // 8 loads in flight per lane before their stores (32 KiB per workgroup), so a workgroup
+        // moves ~10 GB/s or more and the pacing, not the copy loop, sets the rate
+        for (uint32_t i0 = 0; i0 < per; i0 += 8 * 256) {
+            uint4 v[8];
+#pragma unroll
+            for (int u = 0; u < 8; u++) v[u] = src[base + i0 + u * 256 + threadIdx.x];
+#pragma unroll
+            for (int u = 0; u < 8; u++) dst[base + i0 + u * 256 + threadIdx.x] = v[u];
+        }
         __syncthreads();
         if (threadIdx.x == 0) {
             const uint64_t due = t0 + (k + 1) * ticks_per_chunk;
@@ -40,7 +48,7 @@ __global__ __launch_bounds__(256) void paced_copy_kernel(const uint4* __restrict
 extern "C" {
 
 // Move `total_bytes` through `ring_bytes`-sized device buffers (a power of two >= 256 KiB) with `channels` resident
-// workgroups at `gbps` GB/s in all (0: unpaced), on `stream`.  Returns a hipError_t.
+// workgroups of 256 threads at `gbps` GB/s in all (0: unpaced), on `stream`.  Returns a hipError_t.
 int paced_copy(const void* src, void* dst, size_t ring_bytes, size_t total_bytes, int channels, double gbps,
                void* stream) {
     int dev = 0, khz = 0;
