@@ -23,6 +23,7 @@
  *        (LOG_K = log2 of the committed cosets, default LOG_LDE)
  */
 #include <pthread.h>
+#include <dlfcn.h>
 #include <stdint.h>
 #include <stdio.h>
 #include <stdlib.h>
@@ -192,7 +193,8 @@ static void check_commit(uint32_t log_n, uint32_t n_cols, uint32_t log_lde, uint
 /* ------------------------------- 4. collective sharded commit, one thread per rank */
 
 typedef struct {
-    void* group;
+    void* group;            /* in-process transport (bj_comm_init_local), or NULL: */
+    const uint8_t* uid;     /* RCCL (bj_comm_init_rccl) over this unique id */
     int rank, world;
     uint32_t n_cols, log_n, log_lde, log_k, cap;
     const u64* trace; /* all columns, host */
@@ -235,7 +237,7 @@ static void* rank_worker(void* p) {
     HIPC(hipMalloc((void**)&cap, 32 * j->cap));
     for (uint32_t c = 0; c < cpr; c++) HIPC(hipMemcpy(tr + c * n, j->trace + (size_t)cols[c] * n, 8 * n, hipMemcpyHostToDevice));
     bj_comm* comm = NULL;
-    j->rc = bj_comm_init_local(j->group, j->rank, &comm);
+    j->rc = j->group ? bj_comm_init_local(j->group, j->rank, &comm) : bj_comm_init_rccl(j->uid, j->world, j->rank, &comm);
     if (j->rc) return NULL;
     j->rc = bj_sharded_commit_d(comm, tr, n, j->n_cols, j->log_n, j->log_lde, j->log_k, j->cap, BJ_HASHER_POSEIDON2,
                                 lde, leaves, nodes, cap, st);
@@ -251,28 +253,34 @@ static void* rank_worker(void* p) {
     return NULL;
 }
 
-static void check_sharded(uint32_t log_n, uint32_t n_cols, uint32_t log_lde, uint32_t log_k, uint32_t cap, int world) {
+/* use_rccl: the ranks talk through RCCL's API (bj_comm_init_rccl) -- on a one-GPU box only with
+ * the mock librccl.so.1 (tests/c/mock_rccl.cpp, BJ_TEST_MOCK_RCCL), since RCCL refuses two ranks
+ * on one device */
+static void check_sharded(uint32_t log_n, uint32_t n_cols, uint32_t log_lde, uint32_t log_k, uint32_t cap, int world,
+                          int use_rccl) {
     size_t n = (size_t)1 << log_n, nd = n << log_lde, nl = n << log_k, n_nodes = nl - cap;
     u64* trace = xmalloc(8 * n * n_cols);
     for (uint32_t c = 0; c < n_cols; c++)
         for (size_t r = 0; r < n; r++) trace[(size_t)c * n + r] = canon(splitmix64(42 + (u64)c * n + r));
     u64* leaves = xmalloc(32 * nl), *caps = xmalloc(32 * (size_t)cap * world);
     void* group = NULL;
-    int rc = bj_comm_local_group_create(world, &group);
-    CHECK(rc == BJ_OK, "bj_comm_local_group_create: %s", bj_last_error());
+    uint8_t uid[128];
+    int rc = use_rccl ? bj_comm_rccl_unique_id(uid) : bj_comm_local_group_create(world, &group);
+    CHECK(rc == BJ_OK, "%s: %s", use_rccl ? "bj_comm_rccl_unique_id" : "bj_comm_local_group_create", bj_last_error());
     if (rc) return;
     pthread_t th[64];
     rank_job_t jobs[64];
     for (int P = 0; P < world; P++) {
-        jobs[P] = (rank_job_t){group, P, world, n_cols, log_n, log_lde, log_k, cap, trace, leaves,
+        jobs[P] = (rank_job_t){group, uid, P, world, n_cols, log_n, log_lde, log_k, cap, trace, leaves,
                                caps + 4 * (size_t)cap * P, 0};
         pthread_create(&th[P], NULL, rank_worker, &jobs[P]);
     }
     for (int P = 0; P < world; P++) {
         pthread_join(th[P], NULL);
-        CHECK(jobs[P].rc == 0, "rank %d of %d: rc %d", P, world, jobs[P].rc);
+        CHECK(jobs[P].rc == 0, "rank %d of %d%s: rc %d (%s)", P, world, use_rccl ? " (rccl)" : "", jobs[P].rc,
+              bj_last_error());
     }
-    bj_comm_local_group_destroy(group);
+    if (group) bj_comm_local_group_destroy(group);
     u64* r_lde = xmalloc(8 * nd * n_cols), *r_leaves = xmalloc(32 * nl), *r_nodes = xmalloc(32 * n_nodes);
     u64 r_cap[4 * 4096];
     bjo_lde_commit_subset(trace, n_cols, log_n, log_lde, log_k, cap, r_lde, r_leaves, r_nodes, r_cap, 4);
@@ -310,17 +318,27 @@ int main(int argc, char** argv) {
     check_tree_hasher();
     u64 cap_out[4 * 4096];
     check_commit(log_n, n_cols, log_lde, log_k, cap, threads, cap_out);
+    /* BJ_TEST_MOCK_RCCL=path: load the mock librccl.so.1 first, so the library's RCCL path runs
+     * multi-rank on one GPU (the real RCCL refuses two ranks on one device) */
+    const char* mock = getenv("BJ_TEST_MOCK_RCCL");
+    if (mock && !dlopen(mock, RTLD_NOW | RTLD_GLOBAL)) {
+        fprintf(stderr, "cannot load %s: %s\n", mock, dlerror());
+        return 2;
+    }
     for (int world = 2; world <= 8; world *= 2)
-        if (n_cols % world == 0 && ((size_t)1 << (log_n + log_k)) / world > (cap / world ? cap / world : 1))
-            check_sharded(log_n, n_cols, log_lde, log_k, cap, world);
+        if (n_cols % world == 0 && ((size_t)1 << (log_n + log_k)) / world > (cap / world ? cap / world : 1)) {
+            check_sharded(log_n, n_cols, log_lde, log_k, cap, world, 0);
+            if (mock) check_sharded(log_n, n_cols, log_lde, log_k, cap, world, 1);
+        }
     check_errors();
     if (failures) {
         fprintf(stderr, "%d check(s) failed\n", failures);
         return 1;
     }
-    printf("c_caller ok: 2^%u x %u, LDE x%u, %u cosets committed, cap %u, %d seam threads; "
+    printf("c_caller ok%s: 2^%u x %u, LDE x%u, %u cosets committed, cap %u, %d seam threads; "
            "cap[0] = %016llx %016llx %016llx %016llx\n",
-           log_n, n_cols, 1u << log_lde, 1u << log_k, cap, threads, (unsigned long long)canon(cap_out[0]),
+           mock ? " (collective also over RCCL's API, mock librccl)" : "", log_n, n_cols, 1u << log_lde, 1u << log_k, cap,
+           threads, (unsigned long long)canon(cap_out[0]),
            (unsigned long long)canon(cap_out[1]), (unsigned long long)canon(cap_out[2]),
            (unsigned long long)canon(cap_out[3]));
     return 0;

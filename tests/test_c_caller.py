@@ -40,3 +40,23 @@ def test_c_caller(log_n, cols, log_lde, cap, threads, log_k):
                        capture_output=True, text=True, timeout=120)
     assert r.returncode == 0, r.stdout + r.stderr
     assert "c_caller ok" in r.stdout, r.stdout
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("log_n,cols,log_lde,cap,threads,log_k", [
+    (12, 16, 2, 16, 2, 2),    # D = 4: G = 2 all-gather (G < D), 4 (G = D), 8 all-to-all of sender folds (G > D)
+    (13, 16, 3, 32, 2, 1),    # D = 8, k = 2 committed (proof.json's ratio): every block of k cosets
+])
+def test_c_caller_collective_over_rccl_api(log_n, cols, log_lde, cap, threads, log_k):
+    """The collective commit through the library's RCCL code path at G = 2, 4, 8 ranks on one GPU:
+    the mock librccl.so.1 (tests/c/mock_rccl.cpp) gives RCCL's semantics for in-process ranks, so
+    the in-place ncclAllGather offsets, the grouped ncclSend / ncclRecv pairing and their stream
+    ordering are exercised as a multi-GPU run issues them; results checked against the oracle."""
+    _need_bin()
+    mock = os.path.join(ROOT, "tests", "c", "libmock_rccl.so")
+    if not os.path.exists(mock):
+        pytest.fail("tests/c/libmock_rccl.so is not built (run __graft_entry__.build())")
+    r = subprocess.run([BIN, str(log_n), str(cols), str(log_lde), str(cap), str(threads), str(log_k)],
+                       capture_output=True, text=True, timeout=180, env=dict(os.environ, BJ_TEST_MOCK_RCCL=mock))
+    assert r.returncode == 0, r.stdout + r.stderr
+    assert "c_caller ok (collective also over RCCL's API" in r.stdout, r.stdout
