@@ -17,7 +17,8 @@
 // Pass 2  lde3_mid_kernel: scratch block q -> inverse stages R..R+12 -> (optionally the canonical
 //         monomials back to scratch: bj_lde_d's contract) -> per coset: forward stages 0..12
 //         (phases A, B in the power-of-two form, C general) -> 2^R runs of W = 2^(13-R) words,
-//         run T of block q written to [T 8192 + q W, + W) of the coset's column.
+//         run T of block q written to [T 8192 + q' W, + W) of the coset's column, q' = (q mod 32)
+//         2^(R-5) + (q >> 5) (a row rotation, so pass 3 loads its rows contiguously).
 // Pass 3  lde3_final_kernel: region T (8192 contiguous words: rows q < 2^R of W values M =
 //         T W + o) -> the last R forward stages on each M's 2^R values (rows in bit-reversed
 //         order: r = bitrev_R(q)) -> the region in natural order, o 2^R + r.  In place.
@@ -98,6 +99,7 @@ __device__ __forceinline__ u32x2 as_u32x2(uint64_t v) {
     r.y = (uint32_t)(v >> 32);
     return r;
 }
+__device__ __forceinline__ uint64_t from_u32x2(u32x2 v) { return ((uint64_t)v.y << 32) | v.x; }
 
 // x[k] *= f[k] for k < 16
 __device__ __forceinline__ void prescale16(uint64_t* x, const uint64_t* f) {
@@ -161,8 +163,12 @@ __global__ __launch_bounds__(NT, 2) void lde3_mid_kernel(const uint64_t* src, si
     const uint64_t* blk = src + (size_t)c * src_stride + (size_t)q * TILE;
     const uint32_t ba = tail_base_a(t), bc = tail_base_c(t);
     uint64_t x[PT];
+    {
+        const auto rb = uniform_rsrc(blk, 8u * TILE);
 #pragma unroll
-    for (int k = 0; k < PT; k++) x[k] = blk[t + NT * k];
+        for (int k = 0; k < PT; k++)
+            x[k] = from_u32x2(__builtin_amdgcn_raw_buffer_load_b64(rb, (int)(t * 8), k * 2048, 0));
+    }
     if constexpr (INV_PART) {
         // the inverse tail (ct_tail_kernel<., true>): local stages 0..12 of block q, n^-1 in TA
         const uint64_t* ext = inv_tab + ((size_t)1 << LOGN);
@@ -212,9 +218,10 @@ __global__ __launch_bounds__(NT, 2) void lde3_mid_kernel(const uint64_t* src, si
             for (int i = 0; i < 4; i++) lds[bc + k + i] = v[i];
         }
         __syncthreads();
-        uint64_t* mo = mono + (size_t)c * mono_stride + (size_t)q * TILE;
+        const auto rm = uniform_rsrc(mono + (size_t)c * mono_stride + (size_t)q * TILE, 8u * TILE);
 #pragma unroll
-        for (int k = 0; k < PT; k++) mo[t + NT * k] = lds[ba + tail_off_a(k)];
+        for (int k = 0; k < PT; k++)
+            __builtin_amdgcn_raw_buffer_store_b64(as_u32x2(lds[ba + tail_off_a(k)]), rm, (int)(t * 8), k * 2048, 0);
     }
     const uint32_t s8 = brev(t, 8);
     const uint32_t b1 = 33 * t;                                  // phase A out (l-padded)
@@ -222,7 +229,10 @@ __global__ __launch_bounds__(NT, 2) void lde3_mid_kernel(const uint64_t* src, si
     const uint32_t b3 = s8 + (s8 >> 5);                          // phase C read (l-padded)
     const uint32_t g5 = brev(t & 31, 5);                         // phase-B group of this thread
     // store: m = t + 256 k -> run T = (t >> LW) + k 2^(8-LW), word q W + (t & (W-1)) of it
-    const uint32_t vo = ((t >> LW) << 13) + q * W + (t & (W - 1));
+    // rows in the region in rotated order, q' = (q mod 32) 2^(R-5) + (q >> 5): the final pass then
+    // loads its phase-1 rows (q = 32 qh + k, k < 32, per thread) as the contiguous t + 256 k
+    const uint32_t qrot = ((q & 31u) << (R - 5)) | (q >> 5);
+    const uint32_t vo = ((t >> LW) << 13) + qrot * W + (t & (W - 1));
 #pragma unroll 1
     for (uint32_t i = 0; i < n_cosets; i++) {
         const uint64_t* tab = tabs + (size_t)i * tab_stride;
@@ -279,7 +289,8 @@ __global__ __launch_bounds__(NT, 2) void lde3_mid_kernel(const uint64_t* src, si
 
 // ------------------------------------------------------------------- final pass
 //
-// Region T of a coset's column: element (q, o) at q W + o, M = T W + o, r = bitrev_R(q).
+// Region T of a coset's column: element (q, o) at q' W + o (q' the middle pass's row rotation),
+// M = T W + o, r = bitrev_R(q).
 // Phase 1 (stages 13..17, r's top 5 bits = q's low 5): thread (qh = t >> LW, o = t & (W-1)) holds
 // q = 32 qh + k.  Phase 2 (stages 18..12+R, r's low R-5 bits): thread (o, pl = t >> LW) holds
 // groups p = pl + 2^(R-5) h, register h 2^(R-5) + rl <-> r = 2^(R-5) p + rl.  Store: position
@@ -347,12 +358,16 @@ __global__ __launch_bounds__(NT, 2) void lde3_final_kernel(uint64_t* lde, size_t
     const uint32_t T = __builtin_amdgcn_readfirstlane(rest / n_cosets);
     uint64_t* d = lde + (size_t)c * col_stride + (size_t)i * coset_stride + (size_t)T * TILE;
     const uint64_t* tab = tabs + (size_t)i * tab_stride;
-    const uint32_t o = t & (W - 1), qh = t >> LW;
+    const uint32_t o = t & (W - 1);
     const uint32_t M0 = T * W, M = M0 + o;
     uint64_t x[PT], y[PT], f[PT];
-    const uint32_t vi = qh * 32 * W + o;
+    // region rows in the middle pass's rotated order (q' = (q mod 32) 2^(R-5) + (q >> 5)): word t + 256 k
+    // is row q = 32 qh + k (qh = t >> LW), column o -- the phase-1 layout, loaded fully coalesced;
+    // buffer loads (the region's base in SGPRs, 2 KiB steps in soffset): plain loads at
+    // t + 256 k kept a 64-bit VGPR address per register and spilled
+    const auto rd = uniform_rsrc(d, 8u * TILE);
 #pragma unroll
-    for (int k = 0; k < PT; k++) x[k] = d[vi + k * W];
+    for (int k = 0; k < PT; k++) x[k] = from_u32x2(__builtin_amdgcn_raw_buffer_load_b64(rd, (int)(t * 8), k * 2048, 0));
     // table slices into LDS (coalesced: consecutive threads, consecutive M)
     if constexpr (FL::F1_LDS) {
 #pragma unroll
@@ -366,11 +381,13 @@ __global__ __launch_bounds__(NT, 2) void lde3_final_kernel(uint64_t* lde, size_t
     uint64_t g2[F2MODE == 0 && R > 5 ? PT : 1];
     if constexpr (F2MODE == 0 && R > 5) {
         // tabulated phase-2 factors, issued early so their latency overlaps phase 1
-        const uint64_t* f2 = tab + L3_F2 + M + ((size_t)(t >> LW) << 13);
+        // buffer loads: the block's slice base in SGPRs, (32 rl + p) 8192 words in soffset
+        const auto rf = uniform_rsrc(tab + L3_F2 + M0, 8u << (R + 13));
+        const int vf = (int)((o + ((t >> LW) << 13)) * 8);
 #pragma unroll
         for (int k = 0; k < PT; k++) {
             const uint32_t h = k >> RL, rl = k & ((1u << RL) - 1);
-            g2[k] = f2[(size_t)(rl * 32 + (h << RL)) << 13];
+            g2[k] = from_u32x2(__builtin_amdgcn_raw_buffer_load_b64(rf, vf, (int)((rl * 32 + (h << RL)) << 16), 0));
         }
     }
     if constexpr (FL::F1_LDS) {
@@ -422,7 +439,7 @@ __global__ __launch_bounds__(NT, 2) void lde3_final_kernel(uint64_t* lde, size_t
 #pragma unroll
     for (int k = 0; k < PT; k += 4) canon4(y + k);
 #pragma unroll
-    for (int k = 0; k < PT; k++) d[t + NT * k] = y[k];
+    for (int k = 0; k < PT; k++) __builtin_amdgcn_raw_buffer_store_b64(as_u32x2(y[k]), rd, (int)(t * 8), k * 2048, 0);
 }
 
 // ------------------------------------------------------------------- table

@@ -8,7 +8,10 @@ TAG=${1:-r3}
 cd "$GRAFT_REPO_ROOT" && mkdir -p gpurun_out/$TAG && export TMPDIR=/tmp
 O=gpurun_out/$TAG
 L=era-boojum_amd/boojum_amd/libboojum_mi355x.so
-if [ "${2:-}" != "notests" ]; then
+if [ "${2:-}" = "quick" ]; then
+  timeout -k 10 600 python -u -m pytest tests/test_gpu_lde3.py tests/test_gpu_parity.py -m gpu -x -q --timeout 300 --timeout-method thread -k "lde or fft or transforms or commit" > $O/pytest.log 2>&1 || { echo "pytest failed"; grep -E "FAIL|Error" $O/pytest.log | head; tail -20 $O/pytest.log; exit 1; }
+  tail -1 $O/pytest.log
+elif [ "${2:-}" != "notests" ]; then
   timeout -k 10 900 python -u -m pytest tests -m gpu -x -q --timeout 300 --timeout-method thread > $O/pytest.log 2>&1 || { echo "pytest failed"; grep -E "FAIL|Error" $O/pytest.log | head; tail -20 $O/pytest.log; exit 1; }
   tail -1 $O/pytest.log
 fi
