@@ -1,6 +1,7 @@
 """Source hashes of the kernel groups the committed profiles measure.
 
-`__graft_entry__.build()` writes them next to the built library (build_info.json);
+Every library build (`__graft_entry__.build()` and `make -C era-boojum_amd`) writes them next to
+the built library (build_info.json);
 tools/pmc_summary.py stamps every PMC entry with the hash of its group, and bench.py uses a
 committed traffic figure only while the two agree, so a profile can never be quoted for kernels
 it did not measure (host logic only, no device call)."""
@@ -17,7 +18,7 @@ GROUPS = {
     "node_tail_kernel": ("merkle.hip", "poseidon2.hpp", "poseidon2_rc.inc") + _FIELD,
     "b2s_leaf_kernel": ("blake2s.hip",) + _FIELD,
     # the LDE phase: every NTT kernel source and the launch sequence that picks them
-    "lde": ("ntt_ct.hip", "ntt_lde3.hip", "ntt_pow2.hpp", "ntt_dif.hip", "capi.hip") + _FIELD,
+    "lde": ("ntt_ct.hip", "ntt_lde3.hip", "ntt_pow2.hpp", "ntt_dif.hip", "ntt_ct_common.hpp", "capi.hip") + _FIELD,
 }
 
 
@@ -45,3 +46,9 @@ def source_hashes(csrc=CSRC):
 def write_build_info(path):
     with open(path, "w") as f:
         json.dump({"src_hash": source_hashes()}, f, indent=1, sort_keys=True)
+
+
+if __name__ == "__main__":
+    import sys
+
+    write_build_info(sys.argv[1])
