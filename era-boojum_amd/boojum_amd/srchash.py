@@ -18,7 +18,7 @@ GROUPS = {
     "node_tail_kernel": ("merkle.hip", "poseidon2.hpp", "poseidon2_rc.inc") + _FIELD,
     "b2s_leaf_kernel": ("blake2s.hip",) + _FIELD,
     # the LDE phase: every NTT kernel source and the launch sequence that picks them
-    "lde": ("ntt_ct.hip", "ntt_lde3.hip", "ntt_pow2.hpp", "ntt_dif.hip", "ntt_ct_common.hpp", "capi.hip") + _FIELD,
+    "lde": ("ntt.hip", "ntt_ct.hip", "ntt_lde3.hip", "ntt_pow2.hpp", "ntt_dif.hip", "ntt_ct_common.hpp", "capi.hip") + _FIELD,
 }
 
 
