@@ -351,11 +351,15 @@ __global__ __launch_bounds__(NT, 2) void lde3_final_kernel(uint64_t* lde, size_t
     __shared__ uint64_t la[R > 5 && F2MODE == 1 ? FL::A : 1];
     __shared__ uint64_t lu[R > 5 && F2MODE == 1 ? FL::U : 1];
     const uint32_t t = threadIdx.x;
-    // columns fastest: the blocks of one (coset, region) share its table slices in L2
-    const uint32_t c = __builtin_amdgcn_readfirstlane(blockIdx.x % n_cols);
-    const uint32_t rest = blockIdx.x / n_cols;
-    const uint32_t i = __builtin_amdgcn_readfirstlane(rest % n_cosets);
-    const uint32_t T = __builtin_amdgcn_readfirstlane(rest / n_cosets);
+    // columns fastest, XCD-aware: blocks are dealt round-robin over the 8 XCDs, so the n_cols
+    // blocks of one (coset, region) pair sit at ids 8 (pair8 n_cols + c) + (pair & 7), all on one
+    // XCD in one time window, and its table slices are fetched into that XCD's L2 once
+    // (pairs = n_cosets 2^R, a multiple of 8)
+    const uint32_t rest = blockIdx.x >> 3;
+    const uint32_t c = __builtin_amdgcn_readfirstlane(rest % n_cols);
+    const uint32_t pair = ((rest / n_cols) << 3) | (blockIdx.x & 7);
+    const uint32_t i = __builtin_amdgcn_readfirstlane(pair % n_cosets);
+    const uint32_t T = __builtin_amdgcn_readfirstlane(pair / n_cosets);
     uint64_t* d = lde + (size_t)c * col_stride + (size_t)i * coset_stride + (size_t)T * TILE;
     const uint64_t* tab = tabs + (size_t)i * tab_stride;
     const uint32_t o = t & (W - 1);

@@ -2,7 +2,7 @@
 
 The path the reference takes (utils.rs:270-403: iFFT, then D coset FFTs of the same monomials,
 fft/mod.rs:398-411, 659-734) must come out bit for bit: every size the three-pass form serves,
-LDE degrees 2..16, ragged column counts, strided traces, non-canonical inputs, the monomial
+LDE degrees 2..32, ragged column counts, strided traces, non-canonical inputs, the monomial
 scratch contract of bj_lde_d (c_j at bitrev_n(j), canonical), the monomial-source forward pass
 (bj_lde_shard_d, G <= D) and the single-shift pass on folded sub-cosets (G > D).  The two-pass CT
 path (BJ_LDE_PASSES=2, same binary) must agree with it."""
@@ -56,7 +56,7 @@ def lde_d(bj, x, log_d, stride=None):
 
 
 @pytest.mark.parametrize("c,log_n,log_d", [(3, 18, 1), (1, 18, 4), (2, 19, 2), (3, 20, 3), (1, 21, 1), (2, 21, 2),
-                                           (1, 22, 2), (1, 23, 1), (5, 18, 2)])
+                                           (1, 22, 2), (1, 23, 1), (5, 18, 2), (1, 18, 5)])
 def test_lde3_matches_oracle_and_keeps_monomials(bj, c, log_n, log_d):
     x = rand((c, 1 << log_n), 4000 + 10 * log_n + log_d)
     x[0, 0] = np.uint64(2**64 - 1)            # a non-canonical representative
