@@ -34,3 +34,11 @@ def test_stale_traffic_is_withheld():
     assert bench.pmc_traffic(stats, "C3", "lde") == (1.0, False)
     assert bench.pmc_traffic(stats, "C3", "leaf_hash_kernel") == (None, True)
     assert bench.pmc_traffic(stats, "C4", "lde") == (None, None)
+
+
+def test_census_matches_sources():
+    """valu_census.json (the static slot counts bench.py's VALU rooflines use) was made from the
+    kernels in the tree: build() stamps it and regenerates it when a hash differs."""
+    census = json.load(open(os.path.join(ROOT, "era-boojum_amd", "boojum_amd", "valu_census.json")))
+    assert census.get("src_hash") == srchash.source_hashes(), \
+        "valu_census.json is stale: run __graft_entry__.build()"
