@@ -37,6 +37,7 @@ SIGNATURES = {
     "bj_ifft_natural_to_natural_d": ([_vp, _u32, _sz, _u32, _u64, _vp, _vp], _int),
     "bj_ifft_natural_to_natural_h": ([_u64p, _sz, _u64], _int),
     "bj_lde_d": ([_vp, _u32, _sz, _u32, _u32, _vp, _vp, _vp], _int),
+    "bj_lde_ex_d": ([_vp, _u32, _sz, _u32, _u32, _vp, _vp, _u32, _vp], _int),
     "bj_monomials_to_lde_d": ([_vp, _u32, _sz, _u32, _u32, _vp, _vp], _int),
     "bj_lde_coeffs_d": ([_vp, _u32, _sz, _u32, _vp, _sz, _vp], _int),
     "bj_lde_shard_d": ([_vp, _u32, _sz, _u32, _u32, _u32, _u32, _vp, _vp, _vp], _int),

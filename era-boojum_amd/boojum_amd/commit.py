@@ -72,7 +72,7 @@ def witness_commit(trace, lde_degree, cap_size, workspace=None, hasher="poseidon
             raise ValueError("unknown tree hasher %r" % (hasher,))
         _, f_leaves, _, f_nodes = HASHERS[hasher]
         nd, nl = n << log_d, n << log_k
-        call("bj_lde_d", v.data_ptr(), c, stride, log_n, log_d, ws.scratch.data_ptr(), ws.lde.data_ptr(), st)
+        call("bj_lde_ex_d", v.data_ptr(), c, stride, log_n, log_d, ws.scratch.data_ptr(), ws.lde.data_ptr(), 0, st)
         call(f_leaves, ws.lde.data_ptr(), c, nd, nl, ws.leaves.data_ptr(), st)
         call(f_nodes, ws.leaves.data_ptr(), nl, cap_size, ws.nodes.data_ptr(), st)
     ws.hasher = hasher

@@ -42,7 +42,8 @@ def transform_raw_storages_to_lde(trace, lde_degree, scratch=None, out=None):
         scratch = torch.empty((c, n), dtype=torch.int64, device=v.device)
     if out is None:
         out = torch.empty((c, lde_degree, n), dtype=torch.int64, device=v.device)
-    call("bj_lde_d", v.data_ptr(), c, stride, log_n, log_d, scratch.data_ptr(), out.data_ptr(), stream_of(v))
+    # the monomials are not kept (flags 0): scratch is workspace only, as the reference drops them
+    call("bj_lde_ex_d", v.data_ptr(), c, stride, log_n, log_d, scratch.data_ptr(), out.data_ptr(), 0, stream_of(v))
     return out
 
 

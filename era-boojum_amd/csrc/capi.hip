@@ -480,7 +480,7 @@ hipError_t pool_alloc(void** p, size_t bytes, hipStream_t st) {
 extern "C" {
 
 const char* bj_last_error(void) { return g_err.c_str(); }
-uint32_t bj_abi_version(void) { return (2u << 16) | 1u; }
+uint32_t bj_abi_version(void) { return (2u << 16) | 2u; }
 
 int bj_release_workspace(void) {
     HIP_TRY(bj::pool_trim_all(), "hipMemPoolTrimTo");
@@ -598,8 +598,9 @@ int bj_monomials_to_lde_d(const uint64_t* monomials, uint32_t n_cols, size_t mon
     return lde_forward(lde, (size_t)D * n, n, 0, D, monomials, mono_stride, false, n_cols, log_n, log_lde, S(stream));
 }
 
-int bj_lde_d(const uint64_t* trace, uint32_t n_cols, size_t trace_stride, uint32_t log_n, uint32_t log_lde,
-             uint64_t* scratch, uint64_t* lde, void* stream) {
+int bj_lde_ex_d(const uint64_t* trace, uint32_t n_cols, size_t trace_stride, uint32_t log_n, uint32_t log_lde,
+                uint64_t* scratch, uint64_t* lde, uint32_t flags, void* stream) {
+    if (flags & ~BJ_LDE_KEEP_MONOMIALS) return fail(BJ_EINVAL, "unknown bj_lde_ex_d flags");
     if (int r = check_log_n(log_n + log_lde)) return r;
     if (log_lde == 0) return fail(BJ_EINVAL, "lde degree must be > 1 (utils.rs:283)");
     if (n_cols == 0) return BJ_OK;
@@ -607,21 +608,29 @@ int bj_lde_d(const uint64_t* trace, uint32_t n_cols, size_t trace_stride, uint32
     const uint32_t D = 1u << log_lde;
     if (use_lde3(log_n)) {
         // three passes (ntt_lde3.hip): the inverse head into scratch; the inverse tail fused with
-        // forward stages 0..12 of all D cosets (the canonical monomials left in scratch, c_j at
-        // bitrev_n(j)); the last log n - 13 forward stages in place on the LDE
+        // forward stages 0..12 of all D cosets (with BJ_LDE_KEEP_MONOMIALS the canonical
+        // monomials are written back to scratch, c_j at bitrev_n(j)); the last log n - 13 forward
+        // stages in place on the LDE
         const uint64_t *inv, *tabs;
         if (int r = get_ct(log_n, true, 1, &inv)) return r;
         if (int r = get_lde3_lde(log_n, log_lde, &tabs)) return r;
+        uint64_t* mono = (flags & BJ_LDE_KEEP_MONOMIALS) ? scratch : nullptr;
         HIP_TRY(bj::launch_ct_inverse_head(scratch, n, trace, trace_stride, n_cols, log_n, inv, S(stream)), "ifft");
-        HIP_TRY(bj::launch_lde3(lde, (size_t)D * n, n, D, scratch, n, scratch, n, n_cols, log_n, inv, tabs,
+        HIP_TRY(bj::launch_lde3(lde, (size_t)D * n, n, D, scratch, n, mono, n, n_cols, log_n, inv, tabs,
                                 bj::lde3_table_len(log_n), S(stream)),
                 "lde");
         return BJ_OK;
     }
     // iFFT (utils.rs:295-304): scratch = monomials in bit-reversed order; the forward pass
-    // gathers them back in natural order, all D cosets (utils.rs:363-379).
+    // gathers them back in natural order, all D cosets (utils.rs:363-379).  These paths leave
+    // the monomials in scratch with or without the flag.
     if (int r = inverse_to_bitrev(scratch, n, trace, trace_stride, n_cols, log_n, S(stream))) return r;
     return lde_forward(lde, (size_t)D * n, n, 0, D, scratch, n, true, n_cols, log_n, log_lde, S(stream));
+}
+
+int bj_lde_d(const uint64_t* trace, uint32_t n_cols, size_t trace_stride, uint32_t log_n, uint32_t log_lde,
+             uint64_t* scratch, uint64_t* lde, void* stream) {
+    return bj_lde_ex_d(trace, n_cols, trace_stride, log_n, log_lde, scratch, lde, BJ_LDE_KEEP_MONOMIALS, stream);
 }
 
 int bj_lde_coeffs_d(const uint64_t* trace, uint32_t n_cols, size_t trace_stride, uint32_t log_n, uint64_t* coeffs,

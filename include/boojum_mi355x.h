@@ -119,6 +119,15 @@ int bj_ifft_natural_to_natural_h(uint64_t* col, size_t len, uint64_t coset);
 int bj_lde_d(const uint64_t* trace, uint32_t n_cols, size_t trace_stride, uint32_t log_n,
              uint32_t log_lde, uint64_t* scratch, uint64_t* lde, void* stream);
 
+/* bj_lde_d with flags (ABI 2.2).  Without BJ_LDE_KEEP_MONOMIALS, scratch is workspace only and
+ * its contents on return are unspecified -- the reference's transform_raw_storages_to_lde
+ * (utils.rs:270-403) returns the LDE alone and drops the monomials, and the three-pass path
+ * (2^18 <= n <= 2^23) then skips writing them (one pass over n words per column less).
+ * bj_lde_d == bj_lde_ex_d(..., BJ_LDE_KEEP_MONOMIALS, ...).  Unknown flags: BJ_EINVAL. */
+#define BJ_LDE_KEEP_MONOMIALS 1u
+int bj_lde_ex_d(const uint64_t* trace, uint32_t n_cols, size_t trace_stride, uint32_t log_n,
+                uint32_t log_lde, uint64_t* scratch, uint64_t* lde, uint32_t flags, void* stream);
+
 /* Coset LDE of already-monomial columns (transform_monomials_to_lde, utils.rs:311-403;
  * also the quotient commit path prover.rs:1471-1482).  monomials read only. */
 int bj_monomials_to_lde_d(const uint64_t* monomials, uint32_t n_cols, size_t mono_stride, uint32_t log_n,

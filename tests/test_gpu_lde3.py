@@ -123,3 +123,22 @@ def test_lde3_edge_columns(bj):
     m_ref, l_ref = O.lde(x, 3, threads=8)
     eq(got, l_ref.reshape(got.shape))
     assert not got[0].any() and not scratch[0].any()
+
+
+@pytest.mark.parametrize("log_n,log_d", [(18, 1), (20, 2), (22, 2), (23, 1), (17, 2)])
+def test_lde_ex_without_monomials(bj, log_n, log_d):
+    """bj_lde_ex_d without BJ_LDE_KEEP_MONOMIALS: the same LDE as bj_lde_d (the three-pass
+    path then skips writing the monomials; other sizes keep their path); unknown flags refused."""
+    from boojum_amd._lib import call, load
+    c, n = 2, 1 << log_n
+    x = rand((c, n), 4400 + log_n)
+    want, _ = lde_d(bj, x, log_d)
+    t = bj.field.to_device(x)
+    scratch = bj.torch.empty((c, n), dtype=bj.torch.int64, device="cuda")
+    out = bj.torch.empty((c, 1 << log_d, n), dtype=bj.torch.int64, device="cuda")
+    call("bj_lde_ex_d", t.data_ptr(), c, n, log_n, log_d, scratch.data_ptr(), out.data_ptr(), 0,
+         bj.field.stream_of(t))
+    bj.torch.cuda.synchronize()
+    eq(bj.field.to_host(out), want)
+    assert load().bj_lde_ex_d(t.data_ptr(), c, n, log_n, log_d, scratch.data_ptr(), out.data_ptr(), 2,
+                              bj.field.stream_of(t)) == -22
