@@ -25,6 +25,7 @@ SIGNATURES = {
     "bj_last_error": ([], ctypes.c_char_p),
     "bj_abi_version": ([], _u32),
     "bj_release_workspace": ([], _int),
+    "bj_release_tables": ([], _int),
     "bj_prepare": ([_u32], _int),
     "bj_precompute_twiddles_d": ([_u32, _int, _vp, _vp], _int),
     "bj_precompute_twiddles_h": ([_u32, _int, _u64p], _int),

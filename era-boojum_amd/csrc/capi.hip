@@ -480,10 +480,47 @@ hipError_t pool_alloc(void** p, size_t bytes, hipStream_t st) {
 extern "C" {
 
 const char* bj_last_error(void) { return g_err.c_str(); }
-uint32_t bj_abi_version(void) { return (2u << 16) | 2u; }
+uint32_t bj_abi_version(void) { return (2u << 16) | 3u; }
 
 int bj_release_workspace(void) {
     HIP_TRY(bj::pool_trim_all(), "hipMemPoolTrimTo");
+    return BJ_OK;
+}
+
+int bj_release_tables(void) {
+    Cache& c = cache();
+    std::lock_guard<std::mutex> lk(c.mu);
+    int cur = 0;
+    HIP_TRY(hipGetDevice(&cur), "hipGetDevice");
+    // every table, grouped by the device it lives on (the first key element); each device is
+    // synchronised before its tables go, so work already queued on it has finished reading them
+    std::map<int, std::vector<uint64_t*>> per_dev;
+    auto take = [&](auto& m, auto ptr_of) {
+        for (auto& kv : m) per_dev[std::get<0>(kv.first)].push_back(ptr_of(kv.second));
+        m.clear();
+    };
+    auto self = [](uint64_t* p) { return p; };
+    take(c.tw, self);
+    take(c.pyr, self);
+    take(c.pw, [](const std::pair<uint64_t*, uint64_t*>& v) { return v.first; });
+    take(c.lde_pw, self);
+    take(c.ct, self);
+    take(c.ct_lde, self);
+    take(c.lde3, self);
+    take(c.lde3_lde, self);
+    hipError_t first = hipSuccess;
+    for (auto& dv : per_dev) {
+        hipError_t e = hipSetDevice(dv.first);
+        if (e == hipSuccess) e = hipDeviceSynchronize();
+        for (uint64_t* p : dv.second) {
+            const hipError_t f = hipFree(p);
+            if (e == hipSuccess) e = f;
+        }
+        if (first == hipSuccess) first = e;
+    }
+    const hipError_t e = hipSetDevice(cur);
+    if (first == hipSuccess) first = e;
+    if (first != hipSuccess) return hip_fail(first, "bj_release_tables");
     return BJ_OK;
 }
 

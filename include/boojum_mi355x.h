@@ -26,7 +26,8 @@
  * Thread safety: all entry points are re-entrant (the reference calls its FFT seam
  * concurrently from rayon workers, cs/implementations/utils.rs:295-304,363-379).
  * The only global state is a per-device cache of twiddle tables, filled under a
- * lock on first use of a size (bj_prepare fills it ahead of time).
+ * lock on first use of a size (bj_prepare fills it ahead of time; bj_release_tables, which must
+ * not run concurrently with other calls, empties it).
  */
 #ifndef BOOJUM_MI355X_H
 #define BOOJUM_MI355X_H
@@ -51,8 +52,8 @@ uint32_t bj_abi_version(void);
 /* Fill the device twiddle cache for FFT size 2^log_n (forward + inverse tables) on the
  * current device, synchronously.  Twiddle precompute is outside the timed region in
  * the reference's own accounting (prover.rs:313-353 precomputes before "LDE taken").
- * Cached tables are never freed; for 2^13 <= n <= 2^26 a table of one coset shift is
- * n + 1056 (1 + n / 2^13) u64 (36 MiB at 2^22), and an LDE at degree D keeps D of them. */
+ * Cached tables stay until bj_release_tables; for 2^13 <= n <= 2^26 a table of one coset shift
+ * is n + 1056 (1 + n / 2^13) u64 (36 MiB at 2^22), and an LDE at degree D keeps D of them. */
 int bj_prepare(uint32_t log_n);
 
 /* Return the library's cached device workspace to the system (ABI 2.1; no reference
@@ -65,6 +66,16 @@ int bj_prepare(uint32_t log_n);
  * whose stream-ordered free has not completed yet are released by a later call.  Call it when a
  * long-running prover goes idle.  Twiddle tables (bj_prepare) are not affected. */
 int bj_release_workspace(void);
+
+/* Free every cached table (twiddles, coset powers, the LDE passes' factor tables) on every device
+ * (ABI 2.3; no reference counterpart: the reference's twiddles are Vecs the caller drops).  The
+ * cache only grows: an LDE of 2^22 rows at degree 4 keeps ~180 MiB, one of 2^23 at degree 8
+ * ~600 MiB, and a prover that commits many sizes keeps the tables of each.  Each device with
+ * tables is synchronised first, so work already queued there has finished with them; no other
+ * library call may run concurrently with this one, and a HIP graph captured over library calls
+ * holds table addresses, so it must be captured again afterwards.  Later calls rebuild what they
+ * need (as on first use; bj_prepare rebuilds ahead of time). */
+int bj_release_tables(void);
 
 /* ---------------------------------------------------------------- FFT seam */
 

@@ -423,7 +423,7 @@ def test_release_workspace_between_host_commits(bj):
     commit re-allocates its workspace and is still bit-exact."""
     import ctypes
     from boojum_amd._lib import call, load
-    assert load().bj_abi_version() == (2 << 16) | 2
+    assert load().bj_abi_version() == (2 << 16) | 3
     c, log_n, log_d, cap = 40, 14, 2, 16
     tr = O.synthetic_trace(c, log_n)
     ref = O.lde_commit(tr, log_d, cap, threads=8)
@@ -439,6 +439,23 @@ def test_release_workspace_between_host_commits(bj):
         call("bj_release_workspace")
         eq(lde, ref["lde"])
         eq(capo, ref["cap"])
+
+
+def test_release_tables_then_rebuild(bj):
+    """bj_release_tables (ABI 2.3) frees every cached table; the next calls rebuild them: the LDE
+    of both forms (three-pass at 2^18, two-pass CT at 2^14) and a commit stay bit-exact."""
+    from boojum_amd._lib import call
+    from boojum_amd import commit, field
+    for c, log_n, log_d in ((3, 18, 2), (5, 14, 1)):
+        ref = O.lde_commit(O.synthetic_trace(c, log_n), log_d, 16, threads=8)
+        for _ in range(2):
+            tr = commit.synthetic_trace(c, log_n)
+            ws = commit.witness_commit(tr, 1 << log_d, 16)
+            bj.torch.cuda.synchronize()
+            eq(field.to_host(ws.lde), ref["lde"])
+            eq(field.to_host(ws.cap), ref["cap"])
+            del ws, tr
+            call("bj_release_tables")
 
 
 def test_errors_are_loud(bj):
