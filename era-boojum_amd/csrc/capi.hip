@@ -40,10 +40,10 @@ int hip_fail(hipError_t e, const char* what) {
 inline hipStream_t S(void* s) { return reinterpret_cast<hipStream_t>(s); }
 
 // ------------------------------------------------------------ device cache
-// Twiddles per (device, log_n, inverse); power tables per (device, log_n, e, scale).
-// Entries are computed synchronously on a private stream when first inserted, so any
-// caller stream can use them afterwards without ordering concerns; never freed (they are
-// small: n/2 u64 per twiddle table, 4096 + n/4096 u64 per power table).
+// Twiddle, power and LDE factor tables per device and size.  Entries are computed
+// synchronously on a private stream when first inserted, so any caller stream can use them
+// afterwards without ordering concerns; they stay until bj_release_tables (~180 MiB for a
+// 2^22-row LDE at degree 4).
 struct Cache {
     std::mutex mu;
     std::map<std::tuple<int, uint32_t, int>, uint64_t*> tw;
@@ -60,73 +60,85 @@ Cache& cache() {
     return *c;
 }
 
-int get_twiddles(uint32_t log_n, bool inverse, const uint64_t** out) {
-    int dev = 0;
-    HIP_TRY(hipGetDevice(&dev), "hipGetDevice");
-    Cache& c = cache();
-    std::lock_guard<std::mutex> lk(c.mu);
-    auto key = std::make_tuple(dev, log_n, inverse ? 1 : 0);
-    auto it = c.tw.find(key);
-    if (it != c.tw.end()) { *out = it->second; return BJ_OK; }
-    size_t half = log_n ? ((size_t)1 << (log_n - 1)) : 1;
+// A table of `words` u64 on the current device, filled by fill(p, stream) on a private stream and
+// synchronised; nothing is kept on any failure.
+template <class Fill>
+int make_table(size_t words, const char* what, Fill fill, uint64_t** out) {
     uint64_t* p = nullptr;
-    HIP_TRY(hipMalloc(&p, half * sizeof(uint64_t)), "hipMalloc(twiddles)");
+    HIP_TRY(hipMalloc(&p, words * sizeof(uint64_t)), what);
     hipStream_t st;
-    HIP_TRY(hipStreamCreateWithFlags(&st, hipStreamNonBlocking), "hipStreamCreate");
-    hipError_t e = bj::launch_twiddles(p, log_n, inverse, st);
-    if (e == hipSuccess) e = hipStreamSynchronize(st);
-    (void)hipStreamDestroy(st);
-    if (e != hipSuccess) { (void)hipFree(p); return hip_fail(e, "twiddles"); }
-    c.tw[key] = p;
+    hipError_t e = hipStreamCreateWithFlags(&st, hipStreamNonBlocking);
+    if (e == hipSuccess) {
+        e = fill(p, st);
+        if (e == hipSuccess) e = hipStreamSynchronize(st);
+        (void)hipStreamDestroy(st);
+    }
+    if (e != hipSuccess) {
+        (void)hipFree(p);
+        return hip_fail(e, what);
+    }
     *out = p;
     return BJ_OK;
 }
 
+// Look `key` up in `m` under the cache lock, else make and insert the table.
+template <class Map, class Key, class Fill>
+int cached_table(Map& m, const Key& key, size_t words, const char* what, Fill fill, const uint64_t** out) {
+    std::lock_guard<std::mutex> lk(cache().mu);
+    auto it = m.find(key);
+    if (it != m.end()) {
+        *out = it->second;
+        return BJ_OK;
+    }
+    uint64_t* p;
+    if (int r = make_table(words, what, fill, &p)) return r;
+    m[key] = p;
+    *out = p;
+    return BJ_OK;
+}
+
+int current_device(int* dev) {
+    HIP_TRY(hipGetDevice(dev), "hipGetDevice");
+    return BJ_OK;
+}
+
+int get_twiddles(uint32_t log_n, bool inverse, const uint64_t** out) {
+    int dev = 0;
+    if (int r = current_device(&dev)) return r;
+    const size_t half = log_n ? ((size_t)1 << (log_n - 1)) : 1;
+    return cached_table(cache().tw, std::make_tuple(dev, log_n, inverse ? 1 : 0), half, "twiddles",
+                        [&](uint64_t* p, hipStream_t st) { return bj::launch_twiddles(p, log_n, inverse, st); }, out);
+}
+
 int get_powers(uint32_t log_n, uint64_t e_, uint64_t scale, const uint64_t** lo, const uint64_t** hi) {
     int dev = 0;
-    HIP_TRY(hipGetDevice(&dev), "hipGetDevice");
+    if (int r = current_device(&dev)) return r;
     const uint64_t e = gl::canon(e_);
     Cache& c = cache();
     std::lock_guard<std::mutex> lk(c.mu);
     auto key = std::make_tuple(dev, log_n, e, gl::canon(scale));
     auto it = c.pw.find(key);
-    if (it != c.pw.end()) { *lo = it->second.first; *hi = it->second.second; return BJ_OK; }
-    size_t nhi = bj::pw_hi_len(log_n);
-    uint64_t* p = nullptr;
-    HIP_TRY(hipMalloc(&p, (4096 + nhi) * sizeof(uint64_t)), "hipMalloc(powers)");
-    hipStream_t st;
-    HIP_TRY(hipStreamCreateWithFlags(&st, hipStreamNonBlocking), "hipStreamCreate");
-    hipError_t er = bj::launch_power_tables(p, p + 4096, log_n, e, scale, st);
-    if (er == hipSuccess) er = hipStreamSynchronize(st);
-    (void)hipStreamDestroy(st);
-    if (er != hipSuccess) { (void)hipFree(p); return hip_fail(er, "power tables"); }
-    c.pw[key] = {p, p + 4096};
-    *lo = p;
-    *hi = p + 4096;
+    if (it == c.pw.end()) {
+        uint64_t* p;
+        if (int r = make_table(4096 + bj::pw_hi_len(log_n), "power tables", [&](uint64_t* q, hipStream_t st) {
+                return bj::launch_power_tables(q, q + 4096, log_n, e, scale, st);
+            }, &p))
+            return r;
+        it = c.pw.emplace(key, std::make_pair(p, p + 4096)).first;
+    }
+    *lo = it->second.first;
+    *hi = it->second.second;
     return BJ_OK;
 }
 
 // DIF twiddle pyramid (ntt_dif.hip): n entries, TW[m/2 + j] = w_m^j.
 int get_pyramid(uint32_t log_n, bool inverse, const uint64_t** out) {
     int dev = 0;
-    HIP_TRY(hipGetDevice(&dev), "hipGetDevice");
-    Cache& c = cache();
-    std::lock_guard<std::mutex> lk(c.mu);
-    auto key = std::make_tuple(dev, log_n, inverse ? 1 : 0);
-    auto it = c.pyr.find(key);
-    if (it != c.pyr.end()) { *out = it->second; return BJ_OK; }
+    if (int r = current_device(&dev)) return r;
     const size_t n = (size_t)1 << log_n;
-    uint64_t* p = nullptr;
-    HIP_TRY(hipMalloc(&p, (n < 2 ? 2 : n) * sizeof(uint64_t)), "hipMalloc(pyramid)");
-    hipStream_t st;
-    HIP_TRY(hipStreamCreateWithFlags(&st, hipStreamNonBlocking), "hipStreamCreate");
-    hipError_t e = bj::launch_twiddle_pyramid(p, log_n, inverse, st);
-    if (e == hipSuccess) e = hipStreamSynchronize(st);
-    (void)hipStreamDestroy(st);
-    if (e != hipSuccess) { (void)hipFree(p); return hip_fail(e, "pyramid"); }
-    c.pyr[key] = p;
-    *out = p;
-    return BJ_OK;
+    return cached_table(cache().pyr, std::make_tuple(dev, log_n, inverse ? 1 : 0), n < 2 ? 2 : n, "pyramid",
+                        [&](uint64_t* p, hipStream_t st) { return bj::launch_twiddle_pyramid(p, log_n, inverse, st); },
+                        out);
 }
 
 uint64_t lde_coset(uint32_t log_n, uint32_t log_d, uint32_t i);
@@ -135,132 +147,71 @@ uint64_t lde_coset(uint32_t log_n, uint32_t log_d, uint32_t i);
 // [lo 4096 | hi n/4096] for scale * s_i^j (scale = n^-1 when the source is the raw iNTT).
 int get_lde_powers(uint32_t log_n, uint32_t log_d, bool with_ninv, const uint64_t** out, size_t* stride) {
     int dev = 0;
-    HIP_TRY(hipGetDevice(&dev), "hipGetDevice");
+    if (int r = current_device(&dev)) return r;
     const size_t pstride = 4096 + bj::pw_hi_len(log_n);
     *stride = pstride;
-    Cache& c = cache();
-    std::lock_guard<std::mutex> lk(c.mu);
-    auto key = std::make_tuple(dev, log_n, log_d, with_ninv ? 1 : 0);
-    auto it = c.lde_pw.find(key);
-    if (it != c.lde_pw.end()) { *out = it->second; return BJ_OK; }
     const uint32_t D = 1u << log_d;
-    uint64_t* p = nullptr;
-    HIP_TRY(hipMalloc(&p, D * pstride * sizeof(uint64_t)), "hipMalloc(lde powers)");
-    hipStream_t st;
-    HIP_TRY(hipStreamCreateWithFlags(&st, hipStreamNonBlocking), "hipStreamCreate");
     const uint64_t scale = with_ninv ? gl::canon(gl::inv((uint64_t)1 << log_n)) : 1;
-    hipError_t e = hipSuccess;
-    for (uint32_t i = 0; i < D && e == hipSuccess; i++)
-        e = bj::launch_power_tables(p + i * pstride, p + i * pstride + 4096, log_n, lde_coset(log_n, log_d, i), scale,
-                                    st);
-    if (e == hipSuccess) e = hipStreamSynchronize(st);
-    (void)hipStreamDestroy(st);
-    if (e != hipSuccess) { (void)hipFree(p); return hip_fail(e, "lde powers"); }
-    c.lde_pw[key] = p;
-    *out = p;
-    return BJ_OK;
+    return cached_table(cache().lde_pw, std::make_tuple(dev, log_n, log_d, with_ninv ? 1 : 0), D * pstride,
+                        "lde powers", [&](uint64_t* p, hipStream_t st) {
+                            hipError_t e = hipSuccess;
+                            for (uint32_t i = 0; i < D && e == hipSuccess; i++)
+                                e = bj::launch_power_tables(p + i * pstride, p + i * pstride + 4096, log_n,
+                                                            lde_coset(log_n, log_d, i), scale, st);
+                            return e;
+                        }, out);
 }
 
 // Coset-folded CT twiddle table (ntt_ct.hip) for shift s, n entries. The inverse table
 // (s = 1) carries n^-1 in its stage-0 entry.
 int get_ct(uint32_t log_n, bool inverse, uint64_t shift_, const uint64_t** out) {
     int dev = 0;
-    HIP_TRY(hipGetDevice(&dev), "hipGetDevice");
+    if (int r = current_device(&dev)) return r;
     const uint64_t shift = gl::canon(shift_);
-    Cache& c = cache();
-    std::lock_guard<std::mutex> lk(c.mu);
-    auto key = std::make_tuple(dev, log_n, inverse ? 1 : 0, shift);
-    auto it = c.ct.find(key);
-    if (it != c.ct.end()) { *out = it->second; return BJ_OK; }
-    uint64_t* p = nullptr;
-    HIP_TRY(hipMalloc(&p, bj::ct_table_len(log_n) * sizeof(uint64_t)), "hipMalloc(ct table)");
-    hipStream_t st;
-    HIP_TRY(hipStreamCreateWithFlags(&st, hipStreamNonBlocking), "hipStreamCreate");
     const uint64_t scale1 = inverse ? gl::canon(gl::inv((uint64_t)1 << log_n)) : 1;
-    hipError_t e = bj::launch_ct_table(p, log_n, inverse, shift, scale1, st);
-    if (e == hipSuccess) e = hipStreamSynchronize(st);
-    (void)hipStreamDestroy(st);
-    if (e != hipSuccess) { (void)hipFree(p); return hip_fail(e, "ct table"); }
-    c.ct[key] = p;
-    *out = p;
-    return BJ_OK;
+    return cached_table(cache().ct, std::make_tuple(dev, log_n, inverse ? 1 : 0, shift), bj::ct_table_len(log_n),
+                        "ct table", [&](uint64_t* p, hipStream_t st) {
+                            return bj::launch_ct_table(p, log_n, inverse, shift, scale1, st);
+                        }, out);
 }
 
 // The D coset tables of an LDE, table i (shift 7 * w_{nD}^bitrev(i)) at out + i * ct_table_len.
 int get_ct_lde(uint32_t log_n, uint32_t log_d, const uint64_t** out) {
     int dev = 0;
-    HIP_TRY(hipGetDevice(&dev), "hipGetDevice");
-    Cache& c = cache();
-    std::lock_guard<std::mutex> lk(c.mu);
-    auto key = std::make_tuple(dev, log_n, log_d);
-    auto it = c.ct_lde.find(key);
-    if (it != c.ct_lde.end()) { *out = it->second; return BJ_OK; }
+    if (int r = current_device(&dev)) return r;
     const size_t n = bj::ct_table_len(log_n);
     const uint32_t D = 1u << log_d;
-    uint64_t* p = nullptr;
-    HIP_TRY(hipMalloc(&p, D * n * sizeof(uint64_t)), "hipMalloc(ct lde tables)");
-    hipStream_t st;
-    HIP_TRY(hipStreamCreateWithFlags(&st, hipStreamNonBlocking), "hipStreamCreate");
-    hipError_t e = hipSuccess;
-    for (uint32_t i = 0; i < D && e == hipSuccess; i++)
-        e = bj::launch_ct_table(p + i * n, log_n, false, lde_coset(log_n, log_d, i), 1, st);
-    if (e == hipSuccess) e = hipStreamSynchronize(st);
-    (void)hipStreamDestroy(st);
-    if (e != hipSuccess) { (void)hipFree(p); return hip_fail(e, "ct lde tables"); }
-    c.ct_lde[key] = p;
-    *out = p;
-    return BJ_OK;
+    return cached_table(cache().ct_lde, std::make_tuple(dev, log_n, log_d), D * n, "ct lde tables",
+                        [&](uint64_t* p, hipStream_t st) {
+                            hipError_t e = hipSuccess;
+                            for (uint32_t i = 0; i < D && e == hipSuccess; i++)
+                                e = bj::launch_ct_table(p + i * n, log_n, false, lde_coset(log_n, log_d, i), 1, st);
+                            return e;
+                        }, out);
 }
 
 // Three-pass LDE tables (ntt_lde3.hip) of one shift, and of the D coset shifts of an LDE (table i
 // at out + i * lde3_table_len).
 int get_lde3(uint32_t log_n, uint64_t shift_, const uint64_t** out) {
     int dev = 0;
-    HIP_TRY(hipGetDevice(&dev), "hipGetDevice");
+    if (int r = current_device(&dev)) return r;
     const uint64_t shift = gl::canon(shift_);
-    Cache& c = cache();
-    std::lock_guard<std::mutex> lk(c.mu);
-    auto key = std::make_tuple(dev, log_n, shift);
-    auto it = c.lde3.find(key);
-    if (it != c.lde3.end()) { *out = it->second; return BJ_OK; }
-    uint64_t* p = nullptr;
-    HIP_TRY(hipMalloc(&p, bj::lde3_table_len(log_n) * sizeof(uint64_t)), "hipMalloc(lde3 table)");
-    hipStream_t st;
-    HIP_TRY(hipStreamCreateWithFlags(&st, hipStreamNonBlocking), "hipStreamCreate");
-    hipError_t e = bj::launch_lde3_table(p, log_n, shift, st);
-    if (e == hipSuccess) e = hipStreamSynchronize(st);
-    (void)hipStreamDestroy(st);
-    if (e != hipSuccess) { (void)hipFree(p); return hip_fail(e, "lde3 table"); }
-    c.lde3[key] = p;
-    *out = p;
-    return BJ_OK;
+    return cached_table(cache().lde3, std::make_tuple(dev, log_n, shift), bj::lde3_table_len(log_n), "lde3 table",
+                        [&](uint64_t* p, hipStream_t st) { return bj::launch_lde3_table(p, log_n, shift, st); }, out);
 }
-
-uint64_t lde_coset(uint32_t log_n, uint32_t log_d, uint32_t i);
 
 int get_lde3_lde(uint32_t log_n, uint32_t log_d, const uint64_t** out) {
     int dev = 0;
-    HIP_TRY(hipGetDevice(&dev), "hipGetDevice");
-    Cache& c = cache();
-    std::lock_guard<std::mutex> lk(c.mu);
-    auto key = std::make_tuple(dev, log_n, log_d);
-    auto it = c.lde3_lde.find(key);
-    if (it != c.lde3_lde.end()) { *out = it->second; return BJ_OK; }
+    if (int r = current_device(&dev)) return r;
     const size_t L = bj::lde3_table_len(log_n);
     const uint32_t D = 1u << log_d;
-    uint64_t* p = nullptr;
-    HIP_TRY(hipMalloc(&p, D * L * sizeof(uint64_t)), "hipMalloc(lde3 lde tables)");
-    hipStream_t st;
-    HIP_TRY(hipStreamCreateWithFlags(&st, hipStreamNonBlocking), "hipStreamCreate");
-    hipError_t e = hipSuccess;
-    for (uint32_t i = 0; i < D && e == hipSuccess; i++)
-        e = bj::launch_lde3_table(p + i * L, log_n, lde_coset(log_n, log_d, i), st);
-    if (e == hipSuccess) e = hipStreamSynchronize(st);
-    (void)hipStreamDestroy(st);
-    if (e != hipSuccess) { (void)hipFree(p); return hip_fail(e, "lde3 lde tables"); }
-    c.lde3_lde[key] = p;
-    *out = p;
-    return BJ_OK;
+    return cached_table(cache().lde3_lde, std::make_tuple(dev, log_n, log_d), D * L, "lde3 lde tables",
+                        [&](uint64_t* p, hipStream_t st) {
+                            hipError_t e = hipSuccess;
+                            for (uint32_t i = 0; i < D && e == hipSuccess; i++)
+                                e = bj::launch_lde3_table(p + i * L, log_n, lde_coset(log_n, log_d, i), st);
+                            return e;
+                        }, out);
 }
 
 // The three-pass LDE (ntt_lde3.hip) is the default for 2^18..2^23; BJ_LDE_PASSES=2 selects the
