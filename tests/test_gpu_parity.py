@@ -223,6 +223,37 @@ def test_transforms_past_2_23(bj, log_n):
         eq(bj.field.to_host(l), O.lde(x, 1, threads=8)[1])
 
 
+@pytest.mark.slow
+@pytest.mark.parametrize("log_n", [27, 28])
+def test_transforms_past_2_26(bj, log_n):
+    """Columns of 2^27 and 2^28 words (the multi-pass DIF network, ntt_dif.hip), where the oracle
+    does not finish in seconds, checked by closed forms and a round trip: x = e_1 + 5 e_3 gives
+    X_k = c w^k + 5 (c w^k)^3 at bit-reversed position bitrev(k) (4096 sampled positions, coset
+    c = 7), and a device-made random column goes forward (coset 7), back to natural order and
+    through the inverse (coset 7) to itself, bit-exact."""
+    torch = bj.torch
+    n, c = 1 << log_n, 7
+    w = O.domain_generator(log_n)
+    x = torch.zeros((1, n), dtype=torch.int64, device="cuda")
+    x[0, 1], x[0, 3] = 1, 5
+    bj.fft.fft_natural_to_bitreversed(x, c)
+    pos = np.random.default_rng(log_n).integers(0, n, 4096)
+    got = bj.field.to_host(x[0, torch.from_numpy(pos).cuda()])
+    want = []
+    for i in pos.tolist():
+        k = int(format(i, "0%db" % log_n)[::-1], 2)
+        y = O.gl_mul(c, O.gl_pow(w, k))
+        want.append(O.gl_add(y, O.gl_mul(5, O.gl_pow(y, 3))))
+    eq(got, np.array(want, dtype=np.uint64))
+    del x
+    t = bj.commit.synthetic_trace(1, log_n, seed=log_n)
+    ref = t.clone()
+    bj.fft.fft_natural_to_bitreversed(t, c)
+    bj.fft.bitreverse_enumeration_inplace(t)
+    bj.fft.ifft_natural_to_natural(t, c)
+    assert torch.equal(t, ref), "round trip differs"
+
+
 @pytest.mark.parametrize("log_n", [0, 1, 5, 12, 17, 18, 21])
 def test_lde_coeffs_exchange_format(bj, log_n):
     """bj_lde_coeffs_d: monomials c_j at bitrev_n(j), canonical (the multi-GPU exchange format)."""
