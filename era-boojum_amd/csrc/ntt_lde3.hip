@@ -370,13 +370,21 @@ __global__ __launch_bounds__(NT, 2) void lde3_final_kernel(uint64_t* lde, size_t
     // buffer loads (the region's base in SGPRs, 2 KiB steps in soffset): plain loads at
     // t + 256 k kept a 64-bit VGPR address per register and spilled
     const auto rd = uniform_rsrc(d, 8u * TILE);
-#pragma unroll
-    for (int k = 0; k < PT; k++) x[k] = from_u32x2(__builtin_amdgcn_raw_buffer_load_b64(rd, (int)(t * 8), k * 2048, 0));
-    // table slices into LDS (coalesced: consecutive threads, consecutive M)
+    // the F1 slice (coalesced: consecutive threads, consecutive M) is loaded first and stored to
+    // LDS after the region's and F2's loads are issued: loads retire in issue order for vmcnt, so
+    // the LDS stores then wait for these few loads only, and the F2 loads leave with the region's
+    // instead of after all of them have landed
+    constexpr uint32_t NF1 = FL::F1_LDS ? FL::F1 / NT : 1;
+    uint64_t f1v[NF1];
     if constexpr (FL::F1_LDS) {
 #pragma unroll
-        for (uint32_t e = t; e < FL::F1; e += NT) lf1[e] = tab[L3_F1 + ((size_t)(e >> LW) << 13) + M0 + (e & (W - 1))];
+        for (uint32_t j = 0; j < NF1; j++) {
+            const uint32_t e = t + j * NT;
+            f1v[j] = tab[L3_F1 + ((size_t)(e >> LW) << 13) + M0 + (e & (W - 1))];
+        }
     }
+#pragma unroll
+    for (int k = 0; k < PT; k++) x[k] = from_u32x2(__builtin_amdgcn_raw_buffer_load_b64(rd, (int)(t * 8), k * 2048, 0));
     if constexpr (R > 5 && F2MODE == 1) {
         la[t] = tab[L3_A + ((size_t)(t >> LW) << 13) + M0 + (t & (W - 1))];
 #pragma unroll
@@ -395,6 +403,8 @@ __global__ __launch_bounds__(NT, 2) void lde3_final_kernel(uint64_t* lde, size_t
         }
     }
     if constexpr (FL::F1_LDS) {
+#pragma unroll
+        for (uint32_t j = 0; j < NF1; j++) lf1[t + j * NT] = f1v[j];
         __syncthreads();
 #pragma unroll
         for (int k = 0; k < PT; k++) f[k] = lf1[k * W + o];
