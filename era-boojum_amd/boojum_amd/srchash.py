@@ -14,8 +14,8 @@ CSRC = os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))),
 _FIELD = ("gl.hpp", "gl_asm.hpp", "bj_internal.hpp")
 GROUPS = {
     "leaf_hash_kernel": ("merkle.hip", "poseidon2.hpp", "poseidon2_rc.inc") + _FIELD,
-    "node_level_kernel": ("merkle.hip", "poseidon2.hpp", "poseidon2_rc.inc") + _FIELD,
-    "node_tail_kernel": ("merkle.hip", "poseidon2.hpp", "poseidon2_rc.inc") + _FIELD,
+    "node_level_kernel": ("merkle.hip", "poseidon2.hpp", "poseidon2_quad.hpp", "poseidon2_rc.inc") + _FIELD,
+    "node_tail_kernel": ("merkle.hip", "poseidon2.hpp", "poseidon2_quad.hpp", "poseidon2_rc.inc") + _FIELD,
     "b2s_leaf_kernel": ("blake2s.hip",) + _FIELD,
     # the LDE phase: every NTT kernel source and the launch sequence that picks them
     "lde": ("ntt.hip", "ntt_ct.hip", "ntt_lde3.hip", "ntt_pow2.hpp", "ntt_dif.hip", "ntt_ct_common.hpp", "capi.hip") + _FIELD,

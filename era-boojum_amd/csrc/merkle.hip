@@ -13,6 +13,7 @@
 #include <hip/hip_runtime.h>
 #include "gl.hpp"
 #include "poseidon2.hpp"
+#include "poseidon2_quad.hpp"
 #include "bj_internal.hpp"
 
 namespace bj {
@@ -163,6 +164,30 @@ __global__ __launch_bounds__(256) void node_level_kernel(const uint64_t* __restr
     node_hash(lr, lr + 4, next + 4 * i);
 }
 
+// One node per quad of lanes (poseidon2_quad.hpp): for the levels too small to fill the chip,
+// where a level costs one permutation's latency and the quad form shortens it ~2.5x.
+__global__ __launch_bounds__(256) void node_level_q4_kernel(const uint64_t* __restrict__ prev,
+                                                            uint64_t* __restrict__ next, size_t m) {
+    // round constants of the 8 full rounds (rows 0..3, 26..29), each lane reads its own three
+    __shared__ uint64_t rcf[8 * 12];
+    const uint32_t t = threadIdx.x;
+    if (t < 8 * 12) {
+        const uint32_t r = t / 12, e = t % 12, row = r < 4 ? r : r + 22;
+        rcf[t] = p2::RCL.lo[row][e] | (p2::RCL.hi[row][e] << 32);
+    }
+    __syncthreads();
+    const size_t i = (blockIdx.x * (size_t)256 + t) >> 2;
+    const uint32_t p = t & 3;
+    if (i >= m) return;  // whole quads: 4 m lanes
+    const p2q::Consts k = p2q::consts(p);
+    const uint64_t l = prev[8 * i + p], r = prev[8 * i + 4 + p];
+    uint32_t lo[3] = {(uint32_t)l, (uint32_t)r, 0}, hi[3] = {(uint32_t)(l >> 32), (uint32_t)(r >> 32), 0};
+    p2q::permute(lo, hi, rcf, p, k);
+    uint32_t z0, z1;
+    glasm::canon_x1(lo[0], hi[0], z0, z1);
+    next[4 * i + p] = ((uint64_t)z1 << 32) | z0;
+}
+
 // Remaining levels from `len` digests (len <= 4096; launch_nodes hands over len <= 512) down to
 // cap_size, one workgroup.
 __global__ __launch_bounds__(256) void node_tail_kernel(const uint64_t* __restrict__ prev, uint64_t* next,
@@ -240,6 +265,14 @@ hipError_t launch_leaves_chunked(const uint64_t* src, size_t col_stride, uint32_
     return hipGetLastError();
 }
 
+static size_t node_q4_max() {
+    static const size_t v = [] {
+        const char* e = getenv("BJ_NODE_Q4_MAX");
+        return e ? (size_t)strtoull(e, nullptr, 0) : (size_t)1 << 15;
+    }();
+    return v;
+}
+
 hipError_t launch_nodes(const uint64_t* leaves, size_t n_leaves, uint32_t cap_size, uint64_t* nodes,
                         hipStream_t st) {
     const uint64_t* prev = leaves;
@@ -247,10 +280,17 @@ hipError_t launch_nodes(const uint64_t* leaves, size_t n_leaves, uint32_t cap_si
     size_t len = n_leaves;
     // every level above 512 digests as its own grid: a level costs one permutation's latency
     // (~20 us at one wave per SIMD) when every lane hashes one node, while one workgroup
-    // would run a 2048-node level as 8 permutations in sequence
-    while (len > cap_size && len > 512) {
+    // would run a 2048-node level as 8 permutations in sequence.  Levels of <= q4max nodes
+    // (default 2^15: below one wave per SIMD) hash one node per quad of lanes, each level its
+    // own grid down to the cap; BJ_NODE_Q4_MAX=0 keeps one node per lane and the one-workgroup
+    // tail for the last levels.
+    const size_t q4max = node_q4_max();
+    while (len > cap_size && (q4max || len > 512)) {
         size_t m = len / 2;
-        hipLaunchKernelGGL(node_level_kernel, dim3((unsigned)((m + 255) / 256)), dim3(256), 0, st, prev, out, m);
+        if (m <= q4max)
+            hipLaunchKernelGGL(node_level_q4_kernel, dim3((unsigned)((m + 63) / 64)), dim3(256), 0, st, prev, out, m);
+        else
+            hipLaunchKernelGGL(node_level_kernel, dim3((unsigned)((m + 255) / 256)), dim3(256), 0, st, prev, out, m);
         prev = out;
         out += 4 * m;
         len = m;

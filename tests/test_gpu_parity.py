@@ -324,6 +324,31 @@ def test_merkle_tree(bj, c, nl, cap):
         assert bj.merkle.MerkleTreeWithCap.verify_proof_over_cap(path, tree.get_cap(), leaf, idx)
 
 
+def test_node_levels_one_per_lane(bj):
+    """BJ_NODE_Q4_MAX=0 keeps one node per lane for every level and the one-workgroup tail (the
+    form the quad kernel replaces on small levels, poseidon2_quad.hpp); both must give the
+    reference's tree.  A child process, since the library reads the variable once."""
+    import os
+    import subprocess
+    import sys
+    code = (
+        "import numpy as np, oracle as O\n"
+        "from boojum_amd import field, merkle\n"
+        "src = np.random.default_rng(5).integers(0, O.P, size=(9, 1 << 15), dtype=np.uint64)\n"
+        "for cap in (1, 16, 512):\n"
+        "    tree = merkle.MerkleTreeWithCap.construct(field.to_device(src), cap)\n"
+        "    leaves, nodes, levels, capr = O.merkle_construct(src, cap, threads=4)\n"
+        "    assert np.array_equal(field.to_host(tree.nodes), nodes), cap\n"
+        "    assert np.array_equal(tree.get_cap(), capr), cap\n"
+        "print('lane-form tree ok')\n")
+    env = dict(os.environ, BJ_NODE_Q4_MAX="0")
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    env["PYTHONPATH"] = os.pathsep.join([os.path.join(root, "era-boojum_amd"), os.path.join(root, "oracle"),
+                                         env.get("PYTHONPATH", "")])
+    r = subprocess.run([sys.executable, "-c", code], env=env, capture_output=True, text=True, timeout=240)
+    assert r.returncode == 0 and "lane-form tree ok" in r.stdout, r.stdout + r.stderr
+
+
 @pytest.mark.parametrize("c,splits", [(16, [8]), (37, [8, 24]), (256, [64, 128, 192]), (9, [8]), (24, [16])])
 def test_leaves_partial_chain_equals_full(bj, c, splits):
     """bj_merkle_leaves_partial_d over column ranges, carrying the capacity, == bj_merkle_leaves_d."""
