@@ -26,6 +26,8 @@ def group_of(kernel_key):
     """The hash group of a tools/pmc_summary.py kernel key."""
     if kernel_key == "lde" or kernel_key.startswith(("ct_", "dif_", "lde3_")):
         return "lde"
+    if kernel_key == "node_level_q4_kernel":
+        return "node_level_kernel"
     return kernel_key if kernel_key in GROUPS else None
 
 

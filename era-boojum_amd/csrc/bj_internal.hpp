@@ -95,10 +95,13 @@ hipError_t launch_lde3_table(uint64_t* out, uint32_t log_n, uint64_t shift, hipS
 // middle + final passes.  src: inv_tab != NULL -> the inverse head's output (natural order after
 // its log n - 13 stages), and mono (if non-NULL) receives the canonical monomials in bit-reversed
 // order; inv_tab == NULL -> src holds the monomials in bit-reversed order already.  Output coset
-// i (table tabs + i * tab_stride) of column c at lde + c * col_stride + i * coset_stride.
+// i (table tabs + i * tab_stride) of column c at lde + c * col_stride + i * coset_stride; with
+// log_k < log2(n_cosets) the cosets come in blocks of 2^log_k, coset i at
+// lde + c * col_stride + (i >> log_k) * block_stride + (i mod 2^log_k) * coset_stride.
 hipError_t launch_lde3(uint64_t* lde, size_t col_stride, size_t coset_stride, uint32_t n_cosets, const uint64_t* src,
                        size_t src_stride, uint64_t* mono, size_t mono_stride, uint32_t n_cols, uint32_t log_n,
-                       const uint64_t* inv_tab, const uint64_t* tabs, size_t tab_stride, hipStream_t st);
+                       const uint64_t* inv_tab, const uint64_t* tabs, size_t tab_stride, hipStream_t st,
+                       uint32_t log_k = 31, size_t block_stride = 0);
 }  // namespace bj
 
 namespace bj {
@@ -118,4 +121,12 @@ hipError_t pool_trim_all();
 // capi.hip: LDE coset shift 7 * w_{nD}^{bitrev_{log D}(i)} (utils.rs:334-347, 370-373) and the
 // shift of leaf range `shard` of 2^log_shards over the n*D domain, 7 * w_{nD}^{bitrev(shard)}
 uint64_t shard_shift(uint32_t log_n, uint32_t log_lde, uint32_t log_shards, uint32_t shard);
+// capi.hip: the fused three-pass LDE of the trace (bj_lde_ex_d's kernels, no monomial write-back)
+// with the D cosets laid out in blocks of 2^log_k: coset i of column c at
+// lde + (i >> log_k) * block_stride + c * col_stride + (i mod 2^log_k) * 2^log_n.  scratch holds
+// n_cols * 2^log_n words.  False (nothing launched) when log_n is outside the three-pass range.
+bool lde_fused_supported(uint32_t log_n);
+int lde_fused_blocks(const uint64_t* trace, uint32_t n_cols, size_t trace_stride, uint32_t log_n, uint32_t log_lde,
+                     uint32_t log_k, uint64_t* scratch, uint64_t* lde, size_t col_stride, size_t block_stride,
+                     hipStream_t st);
 }  // namespace bj

@@ -378,6 +378,24 @@ int shard_from_folded(const uint64_t* folded, size_t folded_stride, uint32_t n_c
 namespace bj {
 int set_error(int code, const char* msg) { return fail(code, msg); }
 
+bool lde_fused_supported(uint32_t log_n) { return use_lde3(log_n); }
+
+int lde_fused_blocks(const uint64_t* trace, uint32_t n_cols, size_t trace_stride, uint32_t log_n, uint32_t log_lde,
+                     uint32_t log_k, uint64_t* scratch, uint64_t* lde, size_t col_stride, size_t block_stride,
+                     hipStream_t st) {
+    if (!use_lde3(log_n)) return fail(BJ_EINVAL, "internal: fused LDE outside 2^18..2^23");
+    if (n_cols == 0) return BJ_OK;
+    const size_t n = (size_t)1 << log_n;
+    const uint64_t *inv, *tabs;
+    if (int r = get_ct(log_n, true, 1, &inv)) return r;
+    if (int r = get_lde3_lde(log_n, log_lde, &tabs)) return r;
+    HIP_TRY(bj::launch_ct_inverse_head(scratch, n, trace, trace_stride, n_cols, log_n, inv, st), "ifft");
+    HIP_TRY(bj::launch_lde3(lde, col_stride, n, 1u << log_lde, scratch, n, nullptr, 0, n_cols, log_n, inv, tabs,
+                            bj::lde3_table_len(log_n), st, log_k, block_stride),
+            "lde");
+    return BJ_OK;
+}
+
 uint64_t shard_shift(uint32_t log_n, uint32_t log_lde, uint32_t log_shards, uint32_t shard) {
     return ::shard_shift(log_n, log_lde, log_shards, shard);
 }

@@ -157,6 +157,7 @@ struct bj_comm {
     };
     std::vector<Interval> intervals;
     float folded_ms[4] = {0, 0, 0, 0};  // intervals already completed and summed
+    std::string timing_error;           // first failure to read an interval, reported by bj_comm_phase_ms
     int timed_calls = 0;
 };
 
@@ -164,9 +165,9 @@ namespace {
 
 // Sum the intervals whose end event has completed into folded_ms and free their events (all of
 // them when `wait`).  Called at the start of every commit, so a caller that times calls and never
-// reads the totals holds the events of its in-flight calls only.
-int fold_intervals(bj_comm* c, bool wait) {
-    int rc = BJ_OK;
+// reads the totals holds the events of its in-flight calls only.  Timing is bookkeeping: an event
+// that cannot be read is kept as timing_error for bj_comm_phase_ms, never a failure of the commit.
+void fold_intervals(bj_comm* c, bool wait) {
     size_t keep = 0;
     for (size_t i = 0; i < c->intervals.size(); i++) {
         const bj_comm::Interval iv = c->intervals[i];
@@ -177,13 +178,13 @@ int fold_intervals(bj_comm* c, bool wait) {
         }
         float ms = 0;
         if (e == hipSuccess) e = hipEventElapsedTime(&ms, iv.a, iv.b);
-        if (e != hipSuccess && rc == BJ_OK) rc = err(BJ_EHIP, std::string("phase timing: ") + hipGetErrorString(e));
+        if (e != hipSuccess && c->timing_error.empty())
+            c->timing_error = std::string("phase timing: ") + hipGetErrorString(e);
         if (iv.phase >= 0 && iv.phase < 4) c->folded_ms[iv.phase] += ms;
         (void)hipEventDestroy(iv.a);
         (void)hipEventDestroy(iv.b);
     }
     c->intervals.resize(keep);
-    return rc;
 }
 
 // Phase intervals of one timed call (bj_comm_set_timing); a no-op when timing is off.
@@ -538,7 +539,12 @@ int bj_comm_set_timing(bj_comm* c, int on) {
 
 int bj_comm_phase_ms(bj_comm* c, float* ms_out4, int* calls_out) {
     if (!c || !ms_out4) return err(BJ_EINVAL, "null argument");
-    int rc = fold_intervals(c, true);
+    fold_intervals(c, true);
+    int rc = BJ_OK;
+    if (!c->timing_error.empty()) {
+        rc = err(BJ_EHIP, c->timing_error);
+        c->timing_error.clear();
+    }
     for (int i = 0; i < 4; i++) {
         ms_out4[i] = c->folded_ms[i];
         c->folded_ms[i] = 0;
@@ -619,6 +625,8 @@ int bj_sharded_commit_d(bj_comm* comm, const uint64_t* trace_shard, size_t trace
     const bool fold = log_g > log_lde;
     const uint32_t log_f = ls > log_lde ? ls - log_lde : 0;  // folding factor per transform
     const std::vector<Run> runs = column_runs(n_cols, world, rank, hasher);
+    // world 1: no exchange, so no monomials need to reach memory (one run of every column)
+    const bool fused = world == 1 && runs.size() == 1 && bj::lde_fused_supported(log_n);
     const size_t K = runs.size();
     uint32_t max_cc = 0;
     for (const Run& r : runs) max_cc = std::max(max_cc, r.c1 - r.c0);
@@ -642,7 +650,7 @@ int bj_sharded_commit_d(bj_comm* comm, const uint64_t* trace_shard, size_t trace
     }
     std::vector<uint64_t> spm(world);
     // phases 0 inverse (+ fold), 1 lde, 2 leaves, 3 nodes (bj_comm_set_timing)
-    if (!comm->intervals.empty()) BJ_CHECK(fold_intervals(comm, false));
+    if (!comm->intervals.empty()) fold_intervals(comm, false);
     PhaseTimer pt(comm, st);
 
     // 1. local inverse transforms (and folds), each chunk's exchange issued as soon as its
@@ -674,6 +682,7 @@ int bj_sharded_commit_d(bj_comm* comm, const uint64_t* trace_shard, size_t trace
                                     folded + ((size_t)j * n_cols + r.c0) * m, (size_t)r.count * m * 8, xst));
             if (world > 1) HIP_CHECK(hipEventRecord(arrived.ev[k], xs), "hipEventRecord");
         } else {
+            if (fused) continue;  // the inverse runs inside the fused LDE (step 2)
             uint64_t* mine = coeffs + (size_t)r.global * n;
             BJ_CHECK(pt.begin(0));
             BJ_CHECK(bj_lde_coeffs_d(tr, r.count, trace_stride, log_n, mine, n, st));
@@ -696,7 +705,14 @@ int bj_sharded_commit_d(bj_comm* comm, const uint64_t* trace_shard, size_t trace
             uint64_t* out = lde + ((size_t)j * n_cols + r.c0) * m;
             const uint32_t shard = j * world + rank;
             BJ_CHECK(pt.begin(1));
-            if (fold)
+            if (fused) {
+                // one rank, nothing to exchange: bj_lde_ex_d's three passes straight from the trace
+                // (the inverse head, then the inverse tail fused with every coset's first 13 stages),
+                // all B blocks at once
+                if (j == 0)
+                    BJ_CHECK(bj::lde_fused_blocks(trace_shard + (size_t)r.lo * trace_stride, r.count, trace_stride,
+                                                  log_n, log_lde, log_k, coeffs, out, m, (size_t)n_cols * m, st));
+            } else if (fold)
                 BJ_CHECK(bj_lde_shard_folded_d(folded + ((size_t)j * n_cols + r.c0) * m, cc, m, log_n, log_lde, ls,
                                                shard, out, st));
             else

@@ -134,6 +134,13 @@ __device__ __forceinline__ void prescale32_brev_uniform(uint64_t* y, const uint6
     }
 }
 
+// Where coset i of a column starts: (i >> log_k) block_stride + (i mod 2^log_k) coset_stride, i.e.
+// the cosets in blocks of 2^log_k (the collective commit's [block][c][m] layout, m = 2^log_k n);
+// log_k >= log2(n_cosets) is the plain i coset_stride.  Wave-uniform (SGPRs).
+__device__ __forceinline__ size_t coset_offset(uint32_t i, size_t coset_stride, size_t block_stride, uint32_t log_k) {
+    return (size_t)(i >> log_k) * block_stride + (size_t)(i & ((1u << log_k) - 1)) * coset_stride;
+}
+
 // ------------------------------------------------------------------ middle pass
 //
 // LDS layouts of the forward exchanges (element m = position within the block after the
@@ -148,7 +155,7 @@ __device__ __forceinline__ void prescale32_brev_uniform(uint64_t* y, const uint6
 template <int R, bool INV_PART, bool MONO>
 __global__ __launch_bounds__(NT, 2) void lde3_mid_kernel(const uint64_t* src, size_t src_stride, uint64_t* mono,
                                                          size_t mono_stride, uint64_t* lde, size_t col_stride,
-                                                         size_t coset_stride, uint32_t n_cols, uint32_t n_cosets,
+                                                         size_t coset_stride, size_t block_stride, uint32_t log_k, uint32_t n_cols, uint32_t n_cosets,
                                                          const uint64_t* __restrict__ inv_tab,
                                                          const uint64_t* __restrict__ tabs, size_t tab_stride) {
     constexpr uint32_t LOGN = R + 13;
@@ -279,7 +286,7 @@ __global__ __launch_bounds__(NT, 2) void lde3_mid_kernel(const uint64_t* src, si
         // buffer stores: the coset column's base in the descriptor (SGPRs), the per-thread word
         // offset in voffset and each register's run offset k 2^(21 - LW) words in soffset (plain
         // stores made a 64-bit VGPR address per register)
-        const auto rs = uniform_rsrc(lde + (size_t)c * col_stride + (size_t)i * coset_stride, 8u << LOGN);
+        const auto rs = uniform_rsrc(lde + (size_t)c * col_stride + coset_offset(i, coset_stride, block_stride, log_k), 8u << LOGN);
 #pragma unroll
         for (int k = 0; k < PT; k++)
             __builtin_amdgcn_raw_buffer_store_b64(as_u32x2(y[k]), rs, (int)(vo * 8), (int)((uint32_t)k << (24 - LW)),
@@ -340,7 +347,7 @@ struct FinLds {
 };
 
 template <int R, int F2MODE>
-__global__ __launch_bounds__(NT, 2) void lde3_final_kernel(uint64_t* lde, size_t col_stride, size_t coset_stride,
+__global__ __launch_bounds__(NT, 2) void lde3_final_kernel(uint64_t* lde, size_t col_stride, size_t coset_stride, size_t block_stride, uint32_t log_k,
                                                            uint32_t n_cols, uint32_t n_cosets,
                                                            const uint64_t* __restrict__ tabs, size_t tab_stride) {
     using FL = FinLds<R>;
@@ -360,7 +367,7 @@ __global__ __launch_bounds__(NT, 2) void lde3_final_kernel(uint64_t* lde, size_t
     const uint32_t pair = ((rest / n_cols) << 3) | (blockIdx.x & 7);
     const uint32_t i = __builtin_amdgcn_readfirstlane(pair % n_cosets);
     const uint32_t T = __builtin_amdgcn_readfirstlane(pair / n_cosets);
-    uint64_t* d = lde + (size_t)c * col_stride + (size_t)i * coset_stride + (size_t)T * TILE;
+    uint64_t* d = lde + (size_t)c * col_stride + coset_offset(i, coset_stride, block_stride, log_k) + (size_t)T * TILE;
     const uint64_t* tab = tabs + (size_t)i * tab_stride;
     const uint32_t o = t & (W - 1);
     const uint32_t M0 = T * W, M = M0 + o;
@@ -505,21 +512,21 @@ __global__ void lde3_table_kernel(uint64_t* out, uint32_t log_n, uint64_t w_n, u
 }
 
 template <int R>
-void launch_lde3_R(uint64_t* lde, size_t col_stride, size_t coset_stride, uint32_t n_cosets, const uint64_t* src,
+void launch_lde3_R(uint64_t* lde, size_t col_stride, size_t coset_stride, size_t block_stride, uint32_t log_k, uint32_t n_cosets, const uint64_t* src,
                    size_t src_stride, uint64_t* mono, size_t mono_stride, uint32_t n_cols, const uint64_t* inv_tab,
                    const uint64_t* tabs, size_t tab_stride, hipStream_t st) {
     const dim3 gm(n_cols << R);
     if (inv_tab && mono)
         hipLaunchKernelGGL((lde3_mid_kernel<R, true, true>), gm, dim3(NT), 0, st, src, src_stride, mono, mono_stride,
-                           lde, col_stride, coset_stride, n_cols, n_cosets, inv_tab, tabs, tab_stride);
+                           lde, col_stride, coset_stride, block_stride, log_k, n_cols, n_cosets, inv_tab, tabs, tab_stride);
     else if (inv_tab)
         hipLaunchKernelGGL((lde3_mid_kernel<R, true, false>), gm, dim3(NT), 0, st, src, src_stride, mono,
-                           mono_stride, lde, col_stride, coset_stride, n_cols, n_cosets, inv_tab, tabs, tab_stride);
+                           mono_stride, lde, col_stride, coset_stride, block_stride, log_k, n_cols, n_cosets, inv_tab, tabs, tab_stride);
     else
         hipLaunchKernelGGL((lde3_mid_kernel<R, false, false>), gm, dim3(NT), 0, st, src, src_stride, mono,
-                           mono_stride, lde, col_stride, coset_stride, n_cols, n_cosets, inv_tab, tabs, tab_stride);
+                           mono_stride, lde, col_stride, coset_stride, block_stride, log_k, n_cols, n_cosets, inv_tab, tabs, tab_stride);
     const dim3 gf((n_cols * n_cosets) << R);
-    hipLaunchKernelGGL((lde3_final_kernel<R, 0>), gf, dim3(NT), 0, st, lde, col_stride, coset_stride, n_cols,
+    hipLaunchKernelGGL((lde3_final_kernel<R, 0>), gf, dim3(NT), 0, st, lde, col_stride, coset_stride, block_stride, log_k, n_cols,
                        n_cosets, tabs, tab_stride);
 }
 
@@ -543,12 +550,15 @@ hipError_t launch_lde3_table(uint64_t* out, uint32_t log_n, uint64_t shift, hipS
 
 hipError_t launch_lde3(uint64_t* lde, size_t col_stride, size_t coset_stride, uint32_t n_cosets, const uint64_t* src,
                        size_t src_stride, uint64_t* mono, size_t mono_stride, uint32_t n_cols, uint32_t log_n,
-                       const uint64_t* inv_tab, const uint64_t* tabs, size_t tab_stride, hipStream_t st) {
+                       const uint64_t* inv_tab, const uint64_t* tabs, size_t tab_stride, hipStream_t st,
+                       uint32_t log_k, size_t block_stride) {
     if (n_cols == 0 || n_cosets == 0) return hipSuccess;
+    if (log_k > 31) log_k = 31;
     if (!lde3_supported(log_n)) return hipErrorInvalidValue;
-    if (((uint64_t)n_cols * n_cosets) << (log_n - 13) > 0x7fffffffull) return hipErrorInvalidValue;
+    // the final pass's grid: (n_cols n_cosets) 2^R blocks of NT threads, within 2^32 - 1 work-items
+    if (((uint64_t)n_cols * n_cosets) << (log_n - 13) > (0xffffffffull / NT)) return hipErrorInvalidValue;
 #define BJ_LDE3(RR)                                                                                              \
-    launch_lde3_R<RR>(lde, col_stride, coset_stride, n_cosets, src, src_stride, mono, mono_stride, n_cols, inv_tab, \
+    launch_lde3_R<RR>(lde, col_stride, coset_stride, block_stride, log_k, n_cosets, src, src_stride, mono, mono_stride, n_cols, inv_tab, \
                       tabs, tab_stride, st)
     switch (log_n - 13) {
         case 5: BJ_LDE3(5); break;

@@ -17,9 +17,12 @@
  *   4. the collective sharded commit (bj_sharded_commit_d) at G = 2, 4, 8 ranks as threads on
  *      one device, with the same D / k split;
  *   5. the error contract: a violated precondition (fft/mod.rs:399-402 asserts a power-of-two
- *      length) returns BJ_EINVAL with a message, and the library keeps working.
+ *      length) returns BJ_EINVAL with a message, and the library keeps working;
+ *   6. (c_caller release) commits of three sizes, then bj_release_tables + bj_release_workspace
+ *      return the device memory to its baseline.
  *
  * usage: c_caller LOG_N N_COLS LOG_LDE CAP THREADS [LOG_K]   prints "c_caller ok ..." on success
+ *        c_caller release                                    prints "c_caller release ok ..." 
  *        (LOG_K = log2 of the committed cosets, default LOG_LDE)
  */
 #include <pthread.h>
@@ -301,7 +304,54 @@ static void check_errors(void) {
     CHECK(bj_poseidon2_permute_h(st) == BJ_OK, "library unusable after an error: %s", bj_last_error());
 }
 
+/* ------------------- 6. memory returns after the caches are released (ABI 2.1 / 2.3) */
+
+/* Three commits of different sizes leave their tables (per size) and pooled workspace cached;
+ * bj_release_tables + bj_release_workspace (what the Rust shim's BjTables guard runs in its Drop,
+ * INTEGRATION.md) must give the device memory back: free memory returns to its baseline within
+ * `slack` bytes (the runtime's own small allocations).  The reference drops its twiddle Vecs at
+ * scope end (prover.rs:313-353); this is that drop for the library's caches. */
+static void commit_three_sizes(void) {
+    const uint32_t sizes[3][3] = {{16, 16, 1}, {18, 8, 2}, {20, 8, 1}}; /* log_n, cols, log_lde */
+    for (int i = 0; i < 3; i++) {
+        const uint32_t log_n = sizes[i][0], n_cols = sizes[i][1], log_lde = sizes[i][2], cap = 16;
+        const size_t n = (size_t)1 << log_n;
+        u64* trace = xmalloc(8 * n * n_cols);
+        for (size_t j = 0; j < n * n_cols; j++) trace[j] = canon(splitmix64(7 + j));
+        u64 cap_out[4 * 16];
+        int rc = bj_lde_commit_h(trace, n_cols, log_n, log_lde, log_lde, cap, NULL, NULL, NULL, cap_out);
+        CHECK(rc == BJ_OK, "commit 2^%u: rc %d (%s)", log_n, rc, bj_last_error());
+        free(trace);
+    }
+    CHECK(hipDeviceSynchronize() == hipSuccess, "sync");
+}
+
+static void check_release(void) {
+    const size_t slack = (size_t)4 << 20;
+    size_t free0 = 0, free1 = 0, free2 = 0, total = 0;
+    /* a first round, released, so the baseline holds what the runtime keeps once it has run these
+     * kernels at all (code objects, the scratch of spilling kernels, kernel-argument pools,
+     * per-thread streams): only what the library itself caches is measured below */
+    commit_three_sizes();
+    CHECK(bj_release_tables() == BJ_OK && bj_release_workspace() == BJ_OK, "first release: %s", bj_last_error());
+    CHECK(hipMemGetInfo(&free0, &total) == hipSuccess, "hipMemGetInfo");
+    commit_three_sizes();
+    CHECK(hipMemGetInfo(&free1, &total) == hipSuccess, "hipMemGetInfo");
+    CHECK(bj_release_tables() == BJ_OK, "bj_release_tables: %s", bj_last_error());
+    CHECK(bj_release_workspace() == BJ_OK, "bj_release_workspace: %s", bj_last_error());
+    CHECK(hipMemGetInfo(&free2, &total) == hipSuccess, "hipMemGetInfo");
+    CHECK(free1 + ((size_t)16 << 20) < free0, "three commits cached less than 16 MiB (%zu -> %zu)", free0, free1);
+    CHECK(free2 + slack >= free0, "device memory not returned: free %zu before, %zu cached, %zu after release", free0,
+          free1, free2);
+    printf("c_caller release ok: free %.1f MiB before, %.1f with caches, %.1f after release\n", free0 / 1048576.0,
+           free1 / 1048576.0, free2 / 1048576.0);
+}
+
 int main(int argc, char** argv) {
+    if (argc == 2 && strcmp(argv[1], "release") == 0) {
+        check_release();
+        return failures ? 1 : 0;
+    }
     if (argc != 6 && argc != 7) {
         fprintf(stderr, "usage: %s LOG_N N_COLS LOG_LDE CAP THREADS [LOG_K]\n", argv[0]);
         return 2;

@@ -60,3 +60,13 @@ def test_c_caller_collective_over_rccl_api(log_n, cols, log_lde, cap, threads, l
                        capture_output=True, text=True, timeout=180, env=dict(os.environ, BJ_TEST_MOCK_RCCL=mock))
     assert r.returncode == 0, r.stdout + r.stderr
     assert "c_caller ok (collective also over RCCL's API" in r.stdout, r.stdout
+
+
+@pytest.mark.gpu
+def test_c_caller_release_returns_memory():
+    """Commits of three sizes cache tables and workspace; bj_release_tables + bj_release_workspace
+    (the Rust BjTables guard's Drop, integration/rust/ffi.rs) give the device memory back."""
+    _need_bin()
+    r = subprocess.run([BIN, "release"], capture_output=True, text=True, timeout=120)
+    assert r.returncode == 0, r.stdout + r.stderr
+    assert "c_caller release ok" in r.stdout, r.stdout

@@ -10,9 +10,18 @@
   - every node level is spot-checked: sampled parents re-hashed from their two children;
   - the cap recomputed from the level below it;
   - Merkle paths of sampled leaves verify against the cap (verify_proof_over_cap,
-    merkle_tree.rs:482-504).
+    merkle_tree.rs:482-504);
+  - and the whole cap equals the golden cap of the same synthetic trace
+    (tests/golden/bench_caps.json, made by the CPU oracle: tools/make_bench_golden.py), so a
+    fault in any column, row or level shows (get_cap, merkle_tree.rs:451-460).
+* C3 through the collective commit (bj_sharded_commit_d) at G = 4 (whole cosets) and G = 8
+  (sender-folded sub-cosets), the G ranks as threads on this card (bj_comm_local): every rank's
+  all-gathered cap equals the golden C3 cap.
+* C5's shape (93 x 2^16, LDE x8) with Blake2s256 and Poseidon2 trees against their golden caps.
 """
+import json
 import os
+import threading
 
 import numpy as np
 import pytest
@@ -22,6 +31,12 @@ import oracle as O
 pytestmark = [pytest.mark.gpu, pytest.mark.slow]
 
 THREADS = min(16, os.cpu_count() or 1)
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+GOLDEN = json.load(open(os.path.join(ROOT, "tests", "golden", "bench_caps.json")))["caps"]
+
+
+def golden(key):
+    return np.array([[int(x, 16) for x in d] for d in GOLDEN[key]["cap"]], dtype=np.uint64)
 
 
 @pytest.fixture(scope="module")
@@ -66,6 +81,9 @@ def test_fullsize_properties(bj, cfg):
     torch.cuda.synchronize()
     rng = np.random.default_rng(3)
 
+    # the whole cap against the oracle's cap of the same trace
+    eq(bj.field.to_host(ws.cap), golden("C3/poseidon2" if log_n == 22 else "C4/poseidon2"), "golden cap")
+
     # whole columns against the oracle's LDE of the same columns
     cols = [0, c // 2, c - 1]
     x = np.stack([O.synthetic_trace(1, log_n, col_offset=k)[0] for k in cols])
@@ -100,3 +118,62 @@ def test_fullsize_properties(bj, cfg):
     for L in idx[:16]:
         leaf, path = O.merkle_get_proof(leaves, nodes, levels, int(L))
         assert O.verify_proof_over_cap(path, nodes[-cap:], leaf, int(L))
+
+
+@pytest.mark.parametrize("world", [4, 8])
+def test_c3_collective_golden_cap(bj, world):
+    """C3 through bj_sharded_commit_d with G in-process ranks on this card (the native pipeline:
+    chunked exchange on a second stream, per-chunk LDE, sponge continuation, subtree, cap
+    all-gather). G = 4 = D: whole cosets; G = 8 > D: sender-side folds and all-to-alls."""
+    torch = bj.torch
+    from boojum_amd._lib import call
+    from boojum_amd.field import to_host
+    from boojum_amd.sharded import LocalGroup, native_columns, native_sharded_commit
+    c, log_n, log_d, cap = 256, 22, 2, 16
+    torch.cuda.empty_cache()
+    trace = bj.commit.synthetic_trace(c, log_n)
+    torch.cuda.synchronize()
+    group = LocalGroup(world)
+    caps, errors = [None] * world, []
+
+    def rank_main(P):
+        try:
+            torch.cuda.set_device(0)
+            s = torch.cuda.Stream()
+            with torch.cuda.stream(s):
+                cols = torch.tensor(native_columns(c, world, P), device="cuda")
+                shard = trace.index_select(0, cols)
+                comm = group.comm(P)
+                r = native_sharded_commit(comm, shard, c, log_n, log_d, cap)
+                s.synchronize()
+                caps[P] = to_host(r.cap)
+                comm.close()
+                del r, shard
+        except Exception as e:  # noqa: BLE001 - reported below
+            errors.append((P, repr(e)))
+
+    threads = [threading.Thread(target=rank_main, args=(P,), daemon=True) for P in range(world)]
+    for t in threads:
+        t.start()
+    for t in threads:
+        t.join(timeout=100)
+    assert not any(t.is_alive() for t in threads), "a rank did not finish"
+    group.close()
+    del trace
+    torch.cuda.empty_cache()
+    call("bj_release_workspace")
+    assert not errors, errors
+    want = golden("C3/poseidon2")
+    for P in range(world):
+        eq(caps[P], want, "rank %d cap" % P)
+
+
+@pytest.mark.parametrize("hasher", ["blake2s", "poseidon2"])
+def test_c5_shape_golden_cap(bj, hasher):
+    """C5's shape (93 columns x 2^16 rows, LDE x8, cap 16; the sha256 circuit's witness needs
+    the Rust circuit, so the trace is the bench's synthetic one) against its golden cap."""
+    c, log_n, log_d, cap = 93, 16, 3, 16
+    tr = bj.commit.synthetic_trace(c, log_n)
+    ws = bj.commit.witness_commit(tr, 1 << log_d, cap, hasher=hasher)
+    bj.torch.cuda.synchronize()
+    eq(bj.field.to_host(ws.cap), golden("C5/%s" % hasher), "C5 %s cap" % hasher)

@@ -146,6 +146,11 @@ def run_local(torch, world, n_cols, log_n, log_lde, cap, hasher, log_k=None):
     (4, (16, 13, 2, 16, "poseidon2", 0)),   # D = 4, k = 1
     (8, (16, 13, 2, 4, "poseidon2", 0)),    # G > D: sender-side fold per block, cap < G
     (8, (16, 13, 2, 16, "blake2s", 0)),
+    # world 1 in the three-pass range: the fused LDE straight from the trace (no inverse phase),
+    # all blocks of k cosets in one call
+    (1, (16, 18, 2, 16, "poseidon2")),
+    (1, (16, 18, 3, 32, "poseidon2", 1)),
+    (1, (8, 19, 2, 16, "blake2s", 0)),
 ])
 def test_native_sharded_commit_local_ranks(torch_mod, world, cfg):
     n_cols, log_n, log_lde, cap, hasher = cfg[:5]

@@ -29,6 +29,8 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 KERNELS = [
     ("bj::leaf_hash_kernel", "leaf_hash_kernel", 2.0),
     ("bj::node_level_kernel", "node_level_kernel", 1.0),
+    # the small levels (<= 2^15 nodes), one node per quad of lanes: part of the node phase
+    ("bj::node_level_q4_kernel", "node_level_q4_kernel", 1.0),
     ("bj::node_tail_kernel", "node_tail_kernel", 1.0),
     ("bj::(anonymous namespace)::ct_head_kernel<9, 1", "ct_head_fwd", 2.0),
     ("bj::(anonymous namespace)::ct_head_kernel<9, 0", "ct_head_inv", 2.0),

@@ -133,17 +133,19 @@ def ntt_census():
 
 def lde3_census():
     """Per-wave issue slots of the three-pass LDE's kernels (ntt_lde3.hip) for R = log n - 13:
-    the middle pass lde3_mid_kernel<R, true, true> (the inverse tail + monomial store outside its
-    coset loop, one forward stage 0..12 set per loop trip) and the final pass
+    the middle pass lde3_mid_kernel<R, true, false> (the inverse tail outside its coset loop, one
+    forward stage 0..12 set per loop trip; the form bj_lde_ex_d runs without
+    BJ_LDE_KEEP_MONOMIALS, as the bench and the commits do; "mid_mono" is the monomial-storing form) and the final pass
     lde3_final_kernel<R, 0> (no loops).  bench.py prices the LDE phase with them (plus the
     inverse head, head_inv above)."""
     dis = disassemble("ntt_lde3")
     out = {}
     for r in range(5, 11):
-        ins = parse(kernel_lines(dis, "lde3_mid_kernelILi%dELb1ELb1E" % r))
-        if ins:
-            o, body = loop_census(ins)
-            out.setdefault("mid", {})[str(r)] = {"slots_outside_loop": o, "slots_per_coset": body}
+        for key, mono in (("mid", 0), ("mid_mono", 1)):
+            ins = parse(kernel_lines(dis, "lde3_mid_kernelILi%dELb1ELb%dE" % (r, mono)))
+            if ins:
+                o, body = loop_census(ins)
+                out.setdefault(key, {})[str(r)] = {"slots_outside_loop": o, "slots_per_coset": body}
         ins = parse(kernel_lines(dis, "lde3_final_kernelILi%dELi0E" % r))
         if ins:
             v, s = straight_line(ins)
