@@ -64,6 +64,7 @@ SIGNATURES = {
     "bj_keccak256_node_h": ([_u64p, _u64p, _u64p], _int),
     "bj_blake2s_node_h": ([_u64p, _u64p, _u64p], _int),
     "bj_lde_commit_d": ([_vp, _u32, _sz, _u32, _u32, _u32, _u32, _vp, _vp, _vp, _vp, _u64p, _vp], _int),
+    "bj_lde_commit_ex_d": ([_vp, _u32, _sz, _u32, _u32, _u32, _u32, _vp, _vp, _vp, _vp, _u64p, _u32, _vp], _int),
     "bj_lde_commit_h": ([_u64p, _u32, _u32, _u32, _u32, _u32, _u64p, _u64p, _u64p, _u64p], _int),
     "bj_comm_rccl_unique_id": ([_vp], _int),
     "bj_comm_init_rccl": ([_vp, _int, _int, ctypes.POINTER(_vp)], _int),
