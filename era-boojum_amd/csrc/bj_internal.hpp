@@ -18,8 +18,6 @@ hipError_t launch_distribute(uint64_t* cols, size_t col_stride, uint32_t n_cols,
 
 hipError_t launch_leaves(const uint64_t* src, size_t col_stride, uint32_t n_cols, size_t n_leaves, uint64_t* out,
                          hipStream_t st);
-hipError_t launch_leaves_w4(const uint64_t* src, size_t col_stride, uint32_t n_cols, size_t n_leaves, uint64_t* out,
-                            hipStream_t st);
 hipError_t launch_leaves_partial(const uint64_t* src, size_t col_stride, uint32_t n_cols, size_t n_leaves,
                                  const uint64_t* cap_in, uint64_t* out, bool final_, hipStream_t st);
 hipError_t launch_leaves_chunked(const uint64_t* src, size_t col_stride, uint32_t n_cols, uint32_t log_e,
@@ -101,14 +99,12 @@ hipError_t launch_lde3_table(uint64_t* out, uint32_t log_n, uint64_t shift, hipS
 // log_k < log2(n_cosets) the cosets come in blocks of 2^log_k, coset i at
 // lde + c * col_stride + (i >> log_k) * block_stride + (i mod 2^log_k) * coset_stride.
 // parts: LDE3_MID and / or LDE3_FINAL (the final pass of cosets [0, n_cosets) alone reads the
-// middle pass's output in place: src, mono and inv_tab are then unused).  final_lds_pad: dynamic
-// LDS requested per final-pass block on top of its static use (fewer blocks per CU).
+// middle pass's output in place: src, mono and inv_tab are then unused).
 constexpr uint32_t LDE3_MID = 1, LDE3_FINAL = 2;
 hipError_t launch_lde3(uint64_t* lde, size_t col_stride, size_t coset_stride, uint32_t n_cosets, const uint64_t* src,
                        size_t src_stride, uint64_t* mono, size_t mono_stride, uint32_t n_cols, uint32_t log_n,
                        const uint64_t* inv_tab, const uint64_t* tabs, size_t tab_stride, hipStream_t st,
-                       uint32_t log_k = 31, size_t block_stride = 0, uint32_t parts = LDE3_MID | LDE3_FINAL,
-                       uint32_t final_lds_pad = 0);
+                       uint32_t log_k = 31, size_t block_stride = 0, uint32_t parts = LDE3_MID | LDE3_FINAL);
 }  // namespace bj
 
 namespace bj {

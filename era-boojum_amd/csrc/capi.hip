@@ -831,82 +831,9 @@ int bj_keccak256_nodes_d(const uint64_t* leaves, size_t n_leaves, uint32_t cap_s
 }
 
 namespace {
-// The coset pipeline's second stream and its events, per calling thread and device (created once).
-struct PipeCtx {
-    hipStream_t s2 = nullptr;
-    hipEvent_t ev[33] = {};
-};
-int pipe_ctx(PipeCtx** out) {
-    thread_local std::map<std::pair<int, int>, PipeCtx> tl;
-    int dev = 0;
-    HIP_TRY(hipGetDevice(&dev), "hipGetDevice");
-    // BJ_PIPE_PRIO: the second stream's priority (A/B knob; lower is higher priority)
-    const char* pe = getenv("BJ_PIPE_PRIO");
-    const int prio = pe ? atoi(pe) : 0;
-    auto it = tl.find({dev, prio});
-    if (it == tl.end()) {
-        PipeCtx c;
-        HIP_TRY(hipStreamCreateWithPriority(&c.s2, hipStreamNonBlocking, prio), "hipStreamCreate");
-        for (hipEvent_t& e : c.ev) HIP_TRY(hipEventCreateWithFlags(&e, hipEventDisableTiming), "hipEventCreate");
-        it = tl.emplace(std::make_pair(dev, prio), c).first;
-    }
-    *out = &it->second;
-    return BJ_OK;
-}
-
-int env_int(const char* name, int dflt) {
-    const char* e = getenv(name);
-    return e ? atoi(e) : dflt;
-}
-
-// The commit as a coset pipeline (three-pass sizes): the inverse head and the middle pass (all
-// cosets) on st; then the final pass coset by coset on st, each committed coset's leaves hashed
-// on the second stream as soon as its final pass is done (leaf L = coset * n + row, the
-// reference's per-coset leaf order, merkle_tree.rs:112-157), so the VALU-bound hashing of coset
-// i shares the CUs with the latency-bound final passes of cosets i + 1..; the node levels on st
-// once every leaf is in.
-int commit_pipelined(const uint64_t* trace, uint32_t n_cols, size_t trace_stride, uint32_t log_n, uint32_t log_lde,
-                     uint32_t log_k, uint32_t cap_size, uint64_t* scratch, uint64_t* lde, uint64_t* leaves,
-                     uint64_t* nodes, bool keep_mono, hipStream_t st) {
-    const size_t n = (size_t)1 << log_n;
-    const uint32_t D = 1u << log_lde, K = 1u << log_k;
-    PipeCtx* pc;
-    if (int r = pipe_ctx(&pc)) return r;
-    const uint64_t *inv, *tabs;
-    if (int r = get_ct(log_n, true, 1, &inv)) return r;
-    if (int r = get_lde3_lde(log_n, log_lde, &tabs)) return r;
-    const size_t L = bj::lde3_table_len(log_n);
-    const uint32_t pad = (uint32_t)env_int("BJ_FINAL_LDS_PAD", 0);
-    const bool w4 = env_int("BJ_LEAF_W4", 0) != 0;
-    HIP_TRY(bj::launch_ct_inverse_head(scratch, n, trace, trace_stride, n_cols, log_n, inv, st), "ifft");
-    HIP_TRY(bj::launch_lde3(lde, (size_t)D * n, n, D, scratch, n, keep_mono ? scratch : nullptr, n, n_cols, log_n,
-                            inv, tabs, L, st, 31, 0, bj::LDE3_MID),
-            "lde");
-    for (uint32_t i = 0; i < D; i++) {
-        HIP_TRY(bj::launch_lde3(lde + (size_t)i * n, (size_t)D * n, n, 1, nullptr, 0, nullptr, 0, n_cols, log_n,
-                                nullptr, tabs + (size_t)i * L, L, st, 31, 0, bj::LDE3_FINAL, pad),
-                "lde");
-        if (i >= K) continue;
-        HIP_TRY(hipEventRecord(pc->ev[i], st), "hipEventRecord");
-        HIP_TRY(hipStreamWaitEvent(pc->s2, pc->ev[i], 0), "hipStreamWaitEvent");
-        if (w4)
-            HIP_TRY(bj::launch_leaves_w4(lde + (size_t)i * n, (size_t)D * n, n_cols, n, leaves + 4 * (size_t)i * n,
-                                         pc->s2),
-                    "leaves");
-        else
-            HIP_TRY(bj::launch_leaves(lde + (size_t)i * n, (size_t)D * n, n_cols, n, leaves + 4 * (size_t)i * n,
-                                      pc->s2),
-                    "leaves");
-    }
-    HIP_TRY(hipEventRecord(pc->ev[32], pc->s2), "hipEventRecord");
-    HIP_TRY(hipStreamWaitEvent(st, pc->ev[32], 0), "hipStreamWaitEvent");
-    HIP_TRY(bj::launch_nodes(leaves, n << log_k, cap_size, nodes, st), "nodes");
-    return BJ_OK;
-}
-
 int commit_d(const uint64_t* trace, uint32_t n_cols, size_t trace_stride, uint32_t log_n, uint32_t log_lde,
              uint32_t log_commit_cosets, uint32_t cap_size, uint64_t* scratch, uint64_t* lde, uint64_t* leaves,
-             uint64_t* nodes, bool keep_mono, bool pipeline, void* stream) {
+             uint64_t* nodes, bool keep_mono, void* stream) {
     if (log_commit_cosets > log_lde)
         return fail(BJ_EINVAL, "committed cosets exceed the lde degree (prover.rs:313, lde.rs:298-308)");
     if (int r = check_log_n(log_n + log_lde)) return r;
@@ -917,17 +844,11 @@ int commit_d(const uint64_t* trace, uint32_t n_cols, size_t trace_stride, uint32
     const size_t nl = (size_t)1 << (log_n + log_commit_cosets);
     if (!is_pow2(cap_size) || nl <= cap_size)
         return fail(BJ_EINVAL, "need power-of-two cap_size < n * k (merkle_tree.rs:83-96)");
-    if (pipeline && n_cols > 0 && use_lde3(log_n)) {
-        if (int r = commit_pipelined(trace, n_cols, trace_stride, log_n, log_lde, log_commit_cosets, cap_size, scratch,
-                                     lde, leaves, nodes, keep_mono, S(stream)))
-            return r;
-    } else {
-        if (int r = bj_lde_ex_d(trace, n_cols, trace_stride, log_n, log_lde, scratch, lde,
-                                keep_mono ? BJ_LDE_KEEP_MONOMIALS : 0, stream))
-            return r;
-        if (int r = bj_merkle_leaves_d(lde, n_cols, nd, nl, leaves, stream)) return r;
-        if (int r = bj_merkle_nodes_d(leaves, nl, cap_size, nodes, stream)) return r;
-    }
+    if (int r = bj_lde_ex_d(trace, n_cols, trace_stride, log_n, log_lde, scratch, lde,
+                            keep_mono ? BJ_LDE_KEEP_MONOMIALS : 0, stream))
+        return r;
+    if (int r = bj_merkle_leaves_d(lde, n_cols, nd, nl, leaves, stream)) return r;
+    if (int r = bj_merkle_nodes_d(leaves, nl, cap_size, nodes, stream)) return r;
     return BJ_OK;
 }
 }  // namespace
@@ -953,13 +874,9 @@ int bj_lde_commit_d(const uint64_t* trace, uint32_t n_cols, size_t trace_stride,
 int bj_lde_commit_ex_d(const uint64_t* trace, uint32_t n_cols, size_t trace_stride, uint32_t log_n, uint32_t log_lde,
                        uint32_t log_commit_cosets, uint32_t cap_size, uint64_t* scratch, uint64_t* lde,
                        uint64_t* leaves, uint64_t* nodes, uint64_t* cap_h, uint32_t flags, void* stream) {
-    if (flags & ~(BJ_LDE_KEEP_MONOMIALS | BJ_COMMIT_SERIAL | BJ_COMMIT_PIPELINE))
-        return fail(BJ_EINVAL, "unknown bj_lde_commit_ex_d flags");
-    bool pipeline = env_int("BJ_COSET_PIPE", 0) != 0;
-    if (flags & BJ_COMMIT_PIPELINE) pipeline = true;
-    if (flags & BJ_COMMIT_SERIAL) pipeline = false;
+    if (flags & ~BJ_LDE_KEEP_MONOMIALS) return fail(BJ_EINVAL, "unknown bj_lde_commit_ex_d flags");
     if (int r = commit_d(trace, n_cols, trace_stride, log_n, log_lde, log_commit_cosets, cap_size, scratch, lde,
-                         leaves, nodes, (flags & BJ_LDE_KEEP_MONOMIALS) != 0, pipeline, stream))
+                         leaves, nodes, (flags & BJ_LDE_KEEP_MONOMIALS) != 0, stream))
         return r;
     return copy_cap(nodes, (size_t)1 << (log_n + log_commit_cosets), cap_size, cap_h, stream);
 }

@@ -105,15 +105,6 @@ __global__ __launch_bounds__(LEAF_THREADS) void leaf_hash_kernel(const uint64_t*
     leaf_hash_body<HAS_IN, FINAL>(src, col_stride, n_cols, n_leaves, cap_in, out);
 }
 
-// The same hashing held to 128 VGPRs (4 waves per SIMD; it spills a little): two of its waves
-// and one LDE wave fit one SIMD's 512 registers, for the coset pipeline's co-residence A/B
-// (BJ_LEAF_W4=1, capi.hip commit_pipelined)
-__global__ __launch_bounds__(LEAF_THREADS, 4) void leaf_hash_w4_kernel(const uint64_t* __restrict__ src,
-                                                                       size_t col_stride, uint32_t n_cols,
-                                                                       size_t n_leaves, uint64_t* out) {
-    leaf_hash_body<false, true>(src, col_stride, n_cols, n_leaves, nullptr, out);
-}
-
 // Leaf hashing of MerkleTreeWithCap::construct_by_chunking (merkle_tree.rs:176-306) and
 // construct_by_chunking_from_flat_sources (:308-386): leaf L absorbs, for each source column
 // c in order, the E = 2^log_e consecutive elements src[c][L*E .. (L+1)*E).  Used by the FRI
@@ -252,14 +243,6 @@ __global__ __launch_bounds__(256) void permute_kernel(uint64_t* states, size_t c
 hipError_t launch_leaves(const uint64_t* src, size_t col_stride, uint32_t n_cols, size_t n_leaves, uint64_t* out,
                          hipStream_t st) {
     return launch_leaves_partial(src, col_stride, n_cols, n_leaves, nullptr, out, true, st);
-}
-
-hipError_t launch_leaves_w4(const uint64_t* src, size_t col_stride, uint32_t n_cols, size_t n_leaves, uint64_t* out,
-                            hipStream_t st) {
-    if (n_leaves == 0) return hipSuccess;
-    hipLaunchKernelGGL(leaf_hash_w4_kernel, dim3((unsigned)((n_leaves + LEAF_THREADS - 1) / LEAF_THREADS)),
-                       dim3(LEAF_THREADS), 0, st, src, col_stride, n_cols, n_leaves, out);
-    return hipGetLastError();
 }
 
 hipError_t launch_leaves_partial(const uint64_t* src, size_t col_stride, uint32_t n_cols, size_t n_leaves,

@@ -288,15 +288,11 @@ int bj_lde_commit_d(const uint64_t* trace, uint32_t n_cols, size_t trace_stride,
                     uint32_t log_lde, uint32_t log_commit_cosets, uint32_t cap_size, uint64_t* scratch,
                     uint64_t* lde, uint64_t* leaves, uint64_t* nodes, uint64_t* cap_h, void* stream);
 
-/* bj_lde_commit_d with flags (ABI 2.4): BJ_LDE_KEEP_MONOMIALS writes the monomials to scratch
- * (bj_lde_d's contract; without it scratch is workspace only, as transform_raw_storages_to_lde
- * drops them, utils.rs:270-403); BJ_COMMIT_PIPELINE / BJ_COMMIT_SERIAL choose the coset
- * pipeline (the final pass coset by coset on `stream`, each committed coset's leaves hashed on a
- * second stream of the library's as soon as that coset is final, joined back before the node
- * levels) or the phase-serial order; neither flag: the library's default.  Same outputs either
- * way, bit for bit.  bj_lde_commit_d == bj_lde_commit_ex_d(..., BJ_LDE_KEEP_MONOMIALS, ...). */
-#define BJ_COMMIT_SERIAL 2u
-#define BJ_COMMIT_PIPELINE 4u
+/* bj_lde_commit_d with flags (ABI 2.4): with BJ_LDE_KEEP_MONOMIALS scratch receives the
+ * monomials (bj_lde_d's contract); without it scratch is workspace only, as
+ * transform_raw_storages_to_lde drops them (utils.rs:270-403), and the middle LDE pass skips
+ * their write-back.  bj_lde_commit_d == bj_lde_commit_ex_d(..., BJ_LDE_KEEP_MONOMIALS, ...).
+ * Unknown flags: BJ_EINVAL. */
 int bj_lde_commit_ex_d(const uint64_t* trace, uint32_t n_cols, size_t trace_stride, uint32_t log_n,
                        uint32_t log_lde, uint32_t log_commit_cosets, uint32_t cap_size, uint64_t* scratch,
                        uint64_t* lde, uint64_t* leaves, uint64_t* nodes, uint64_t* cap_h, uint32_t flags,

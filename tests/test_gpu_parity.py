@@ -450,6 +450,41 @@ def test_witness_commit_matches_oracle(bj, c, log_n, log_d, cap, log_k):
     eq(bj.field.to_host(ws.cap), ref["cap"])
 
 
+@pytest.mark.parametrize("c,log_n,log_d,log_k", [(24, 18, 2, 1), (5, 12, 1, 1)])
+def test_lde_commit_ex_flags(bj, c, log_n, log_d, log_k):
+    """bj_lde_commit_ex_d (ABI 2.4): flags 0 commits like bj_lde_commit_d without writing the
+    monomials back (three-pass size and a two-pass one); BJ_LDE_KEEP_MONOMIALS leaves them in
+    scratch as bj_lde_d does; unknown flags are refused."""
+    import ctypes
+    from boojum_amd._lib import call, load
+    torch = bj.torch
+    cap = 16
+    n, D = 1 << log_n, 1 << log_d
+    nl = n << log_k
+    tr_np = O.synthetic_trace(c, log_n)
+    tr = bj.commit.synthetic_trace(c, log_n)
+    ref = O.lde_commit(tr_np, log_d, cap, threads=8, log_k=log_k)
+    st = bj.field.stream_of(tr)
+    for flags in (0, 1):
+        scratch = torch.zeros((c, n), dtype=torch.int64, device="cuda")
+        lde = torch.empty((c, D, n), dtype=torch.int64, device="cuda")
+        leaves = torch.empty((nl, 4), dtype=torch.int64, device="cuda")
+        nodes = torch.empty((nl - cap, 4), dtype=torch.int64, device="cuda")
+        capo = np.zeros((cap, 4), dtype=np.uint64)
+        call("bj_lde_commit_ex_d", tr.data_ptr(), c, n, log_n, log_d, log_k, cap, scratch.data_ptr(), lde.data_ptr(),
+             leaves.data_ptr(), nodes.data_ptr(), capo.ctypes.data_as(ctypes.POINTER(ctypes.c_uint64)), flags, st)
+        torch.cuda.synchronize()
+        eq(bj.field.to_host(lde), ref["lde"])
+        eq(bj.field.to_host(leaves), ref["leaves"])
+        eq(bj.field.to_host(nodes), ref["nodes"])
+        eq(capo, ref["cap"])
+        if flags:
+            m_ref, _ = O.lde(tr_np, log_d, threads=8)
+            eq(bj.field.to_host(scratch), np.stack([O.bitreverse(m_ref[i]) for i in range(c)]))
+    assert load().bj_lde_commit_ex_d(tr.data_ptr(), c, n, log_n, log_d, log_k, cap, scratch.data_ptr(),
+                                     lde.data_ptr(), leaves.data_ptr(), nodes.data_ptr(), None, 2, st) == -22
+
+
 @pytest.mark.parametrize("c,log_n,log_d,cap,log_k", [(5, 8, 2, 4, 2), (70, 10, 1, 16, 1), (64, 12, 2, 8, 2),
                                                      (33, 14, 3, 16, 3), (40, 14, 3, 32, 1), (20, 12, 2, 16, 0)])
 def test_commit_host_abi_matches(bj, c, log_n, log_d, cap, log_k):
