@@ -38,7 +38,7 @@ namespace bj {
 namespace {
 
 // table of one coset shift s (launch_lde3_table), for log n = R + 13:
-//   [0, 8192)            CT13[2^u + g] = s^(n >> (u+1)) w_{2^(u+1)}^bitrev_u(g), u < 13 (forward phase C)
+//   [L3_C, +8192)        sigma_10(G)^((n/8192) j) at 8 G + j                    (forward phase C)
 //   [L3_HA, +32)         s^((n/32) k)                                  (forward phase A)
 //   [L3_HB, +1024)       sigma_5(g)^((n/1024) k) at 32 g + k            (forward phase B)
 //   [L3_F1, +2^18)       sigma_13(M)^(2^(R-5) k) at k 8192 + M          (final phase 1)
@@ -49,6 +49,7 @@ namespace {
 // sigma_18(32 M + p)^rl = A[rl][M] U[p][rl], since sigma_18(32 M + p) = sigma_13(M) w_{2^R}^bitrev_5(p).
 // F1, A and F2 are laid out M-fastest, so the W lanes of a final block that share a row read
 // consecutive words.
+constexpr size_t L3_C = 0;
 constexpr size_t L3_HA = 8192;
 constexpr size_t L3_HB = L3_HA + 32;
 constexpr size_t L3_F1 = L3_HB + 1024;
@@ -131,6 +132,34 @@ __device__ __forceinline__ void prescale32_brev_uniform(uint64_t* y, const uint6
                          (uint32_t)a3, (uint32_t)(a3 >> 32), (uint32_t)f3, (uint32_t)(f3 >> 32), z0[3], z1[3]);
 #pragma unroll
         for (int i = 0; i < 4; i++) y[k + i] = join2(z0[i], z1[i]);
+    }
+}
+
+// Phase C's factors of the middle pass, k = 8 g + j with j > 0 (j = 0 is 1): loaded to f[k]
+__device__ __forceinline__ void load28_c(uint64_t* f, const uint64_t* __restrict__ c) {
+#pragma unroll
+    for (int k = 0; k < PT; k++)
+        if (k & 7) f[k] = c[k];
+}
+
+// y[k] *= f[k] for the 28 registers k mod 8 != 0 (general products)
+__device__ __forceinline__ void prescale28_c(uint64_t* y, const uint64_t* f) {
+#pragma unroll
+    for (int q = 0; q < 7; q++) {
+        int k[4];
+#pragma unroll
+        for (int i = 0; i < 4; i++) {
+            const int e = 4 * q + i;         // e-th of the 28: group e / 7, j = e % 7 + 1
+            k[i] = 8 * (e / 7) + e % 7 + 1;
+        }
+        uint32_t z0[4], z1[4];
+        glasm::mul_x4((uint32_t)y[k[0]], (uint32_t)(y[k[0]] >> 32), (uint32_t)f[k[0]], (uint32_t)(f[k[0]] >> 32), z0[0],
+                      z1[0], (uint32_t)y[k[1]], (uint32_t)(y[k[1]] >> 32), (uint32_t)f[k[1]],
+                      (uint32_t)(f[k[1]] >> 32), z0[1], z1[1], (uint32_t)y[k[2]], (uint32_t)(y[k[2]] >> 32),
+                      (uint32_t)f[k[2]], (uint32_t)(f[k[2]] >> 32), z0[2], z1[2], (uint32_t)y[k[3]],
+                      (uint32_t)(y[k[3]] >> 32), (uint32_t)f[k[3]], (uint32_t)(f[k[3]] >> 32), z0[3], z1[3]);
+#pragma unroll
+        for (int i = 0; i < 4; i++) y[k[i]] = join2(z0[i], z1[i]);
     }
 }
 
@@ -264,19 +293,19 @@ __global__ __launch_bounds__(NT, 2) void lde3_mid_kernel(const uint64_t* src, si
         for (int k = 16; k < PT; k++) f[k] = hb[k];
         prescale16(y + 16, f + 16);
         dft_p2<5, false, 0>(y);
-        uint64_t wa[16], wb[16], wc[16];
-        tw_ct_tailC<10>(wa, tab, 0, 0, t);
 #pragma unroll
         for (int k = 0; k < PT; k++) lds[b2 + 33 * cbrev(k, 5)] = y[k];
-        tw_ct_tailC<11>(wb, tab, 0, 0, t);
-        tw_ct_tailC<12>(wc, tab, 0, 0, t);
+        // phase C's factors (28: the first of each group of 8 is 1), issued before the barrier
+        load28_c(f, tab + L3_C + 32 * t);
         __syncthreads();
 #pragma unroll
         for (int k = 0; k < PT; k++) y[k] = lds[b3 + 264 * cbrev(k, 5)];
-        // phase C (stages 10..12), general twiddles CT13[2^u + (m >> (13 - u))]
-        ct_stage<4>(y, wa);
-        ct_stage<2>(y, wb);
-        ct_stage<1>(y, wc);
+        // phase C (stages 10..12) as a power-of-two phase: the 8 elements m = 8 G + j of stage-10
+        // group G = 4 t + (k >> 3) times sigma_10(G)^((n / 8192) j), then an 8-point DFT with w_8
+        // (the CT network's twiddles CT13[2^u + (m >> (13 - u))] are these factors' powers
+        // times 8th roots of unity)
+        prescale28_c(y, f);
+        dft_p2_groups<3, false>(y);
         __syncthreads();
 #pragma unroll
         for (int k = 0; k < PT; k++) lds[bc + k] = y[k];
@@ -471,14 +500,9 @@ __global__ void lde3_table_kernel(uint64_t* out, uint32_t log_n, uint64_t w_n, u
          idx += (size_t)gridDim.x * blockDim.x) {
         uint64_t v;
         if (idx < L3_HA) {
-            if (idx == 0) {
-                v = 0;
-            } else {
-                const uint32_t u = 31 - __builtin_clz((uint32_t)idx);
-                const uint32_t g = (uint32_t)idx - (1u << u);
-                const uint64_t e = (uint64_t)gl::bitrev32(g, u) << (log_n - u - 1);
-                v = gl::mul(gl::pow(w_n, e), gl::pow(s, n >> (u + 1)));
-            }
+            const uint32_t G = (uint32_t)idx >> 3, j = (uint32_t)idx & 7;
+            const uint64_t sigma = gl::mul(s, gl::pow(w_n, gl::bitrev32(G, 10)));
+            v = gl::pow(sigma, (n >> 13) * j);
         } else if (idx < L3_HB) {
             v = gl::pow(s, (n >> 5) * (idx - L3_HA));
         } else if (idx < L3_F1) {
