@@ -76,22 +76,34 @@ __device__ __forceinline__ void leaf_hash_body(const uint64_t* __restrict__ src,
 #pragma unroll
         for (int i = 0; i < 8; i++) nxt[i] = p[(size_t)i * col_stride];
     }
-    for (uint32_t g = 0; g < full; g++) {
+    // every absorption but the leaf's last is followed by another, which overwrites words 0..7:
+    // it needs the capacity words only; the last needs the digest (FINAL) or the capacity.  The
+    // last full group is peeled out of the loop (no prefetch live across its permutation).
+    if (full > 0) {
+        for (uint32_t g = 0; g + 1 < full; g++) {
+#pragma unroll
+            for (int i = 0; i < 8; i++) {
+                s.lo[i] = (uint32_t)nxt[i];
+                s.hi[i] = (uint32_t)(nxt[i] >> 32);
+            }
+            const uint64_t* q = p + (size_t)(g + 1) * 8 * col_stride;
+#pragma unroll
+            for (int i = 0; i < 8; i++) nxt[i] = q[(size_t)i * col_stride];
+            p2::permute<p2::OUT_CAP>(s);
+        }
 #pragma unroll
         for (int i = 0; i < 8; i++) {
             s.lo[i] = (uint32_t)nxt[i];
             s.hi[i] = (uint32_t)(nxt[i] >> 32);
         }
-        if (g + 1 < full) {
-            const uint64_t* q = p + (size_t)(g + 1) * 8 * col_stride;
-#pragma unroll
-            for (int i = 0; i < 8; i++) nxt[i] = q[(size_t)i * col_stride];
-        }
-        p2::permute(s);
+        if (FINAL && rem == 0)
+            p2::permute<p2::OUT_DIGEST>(s);
+        else
+            p2::permute<p2::OUT_CAP>(s);
     }
     if (FINAL && rem) {
         load8(s, p + (size_t)full * 8 * col_stride, col_stride, rem);
-        p2::permute(s);
+        p2::permute<p2::OUT_DIGEST>(s);
     }
     if (FINAL) store_canon4(s, out + 4 * L);
     else store_canon4_at(s, 2, out + 4 * L);
@@ -122,8 +134,10 @@ __global__ __launch_bounds__(LEAF_THREADS) void leaf_chunk_kernel(const uint64_t
 #pragma unroll
     for (int i = 0; i < 12; i++) s.lo[i] = s.hi[i] = 0;
     const uint32_t total = n_cols << log_e;
+    // every group but the last is followed by another (capacity words only); the last, full or
+    // zero-padded, gives the digest
     uint32_t k = 0;
-    for (; k + 8 <= total; k += 8) {
+    for (; k + 8 < total; k += 8) {
 #pragma unroll
         for (int i = 0; i < 8; i++) {
             const uint32_t e = k + i;
@@ -131,7 +145,7 @@ __global__ __launch_bounds__(LEAF_THREADS) void leaf_chunk_kernel(const uint64_t
             s.lo[i] = (uint32_t)v;
             s.hi[i] = (uint32_t)(v >> 32);
         }
-        p2::permute(s);
+        p2::permute<p2::OUT_CAP>(s);
     }
     if (k < total) {
 #pragma unroll
@@ -141,7 +155,7 @@ __global__ __launch_bounds__(LEAF_THREADS) void leaf_chunk_kernel(const uint64_t
             s.lo[i] = (uint32_t)v;
             s.hi[i] = (uint32_t)(v >> 32);
         }
-        p2::permute(s);
+        p2::permute<p2::OUT_DIGEST>(s);
     }
     store_canon4(s, out + 4 * L);
 }
@@ -156,7 +170,7 @@ __device__ __forceinline__ void node_hash(const uint64_t* l, const uint64_t* r, 
         s.hi[4 + i] = (uint32_t)(r[i] >> 32);
         s.lo[8 + i] = s.hi[8 + i] = 0;
     }
-    p2::permute(s);
+    p2::permute<p2::OUT_DIGEST>(s);
     store_canon4(s, o);
 }
 

@@ -85,6 +85,13 @@ __device__ __forceinline__ void m4_limbs(uint64_t& x0, uint64_t& x1, uint64_t& x
     x0 = t6; x1 = t5; x2 = t7; x3 = t4;
 }
 
+// Which outputs of a permutation its caller reads: all 12 (bj_poseidon2_permute), the capacity
+// words 8..11 (a sponge absorption followed by another: the Overwrite sponge replaces words 0..7,
+// sponge.rs:241-323), or the digest words 0..3 (the last absorption of a leaf, a node).  The
+// last round's external MDS and the final reduction then form only those outputs.
+enum Out { OUT_ALL = 0, OUT_CAP = 1, OUT_DIGEST = 2 };
+
+template <int OUT = OUT_ALL>
 __device__ __forceinline__ void mds_ext_limbs(const uint32_t* v, uint64_t* X) {
 #pragma unroll
     for (int i = 0; i < 12; i++) X[i] = v[i];
@@ -94,10 +101,16 @@ __device__ __forceinline__ void mds_ext_limbs(const uint32_t* v, uint64_t* X) {
 #pragma unroll
     for (int i = 0; i < 4; i++) {
         uint64_t a = X[i], b = X[i + 4], c = X[i + 8];
-        uint64_t s = a + b + c;
-        X[i] = s + a;
-        X[i + 4] = s + b;
-        X[i + 8] = s + c;
+        if constexpr (OUT == OUT_ALL) {
+            uint64_t s = a + b + c;
+            X[i] = s + a;
+            X[i + 4] = s + b;
+            X[i + 8] = s + c;
+        } else if constexpr (OUT == OUT_CAP) {
+            X[i + 8] = (c << 1) + a + b;
+        } else {
+            X[i] = (a << 1) + b + c;
+        }
     }
 }
 
@@ -108,9 +121,12 @@ __device__ __forceinline__ void split(uint64_t z, uint32_t& lo, uint32_t& hi) {
 
 // (L, H) -> reduced (lo, hi) for all 12 elements.  The reductions write 64-bit register pairs;
 // lo / hi are their halves (sub-registers, no moves).
+template <int OUT = OUT_ALL>
 __device__ __forceinline__ void reduce12(const uint64_t* L, const uint64_t* H, uint32_t* lo, uint32_t* hi) {
 #pragma unroll
     for (int q = 0; q < 3; q++) {
+        if constexpr (OUT == OUT_CAP) { if (q != 2) continue; }
+        if constexpr (OUT == OUT_DIGEST) { if (q != 0) continue; }
         const int i = 4 * q;
         uint64_t z[4];
         glasm::reduce_x4(L[i], (uint32_t)H[i], (uint32_t)(H[i] >> 32), z[0],
@@ -125,6 +141,7 @@ __device__ __forceinline__ void reduce12(const uint64_t* L, const uint64_t* H, u
 // Full round r on the pending limbs (L, H) of the state (the external MDS of the previous
 // step not yet reduced): reduce(L + RC_r, H + RC_r), x^7, then the external MDS into
 // new pending limbs.  Leaves the reduced S-box output in s.
+template <int OUT = OUT_ALL>
 __device__ __forceinline__ void full_round(State& s, uint64_t* L, uint64_t* H, int r) {
 #pragma unroll
     for (int i = 0; i < 12; i++) {
@@ -134,8 +151,8 @@ __device__ __forceinline__ void full_round(State& s, uint64_t* L, uint64_t* H, i
     reduce12(L, H, s.lo, s.hi);
 #pragma unroll
     for (int q = 0; q < 3; q++) sbox_x4(s.lo + 4 * q, s.hi + 4 * q);
-    mds_ext_limbs(s.lo, L);
-    mds_ext_limbs(s.hi, H);
+    mds_ext_limbs<OUT>(s.lo, L);
+    mds_ext_limbs<OUT>(s.hi, H);
 }
 
 // lo + b as a 64-bit limb in one v_mad_u64_u32 (lo * 1 + b): no zero-extended register pair
@@ -174,7 +191,9 @@ __device__ __forceinline__ void partial_round_pair(uint64_t* Z, int r) {
 }
 
 // The permutation (state_generic_impl.rs:221-236): MDS; 4 x (RC, S-box, MDS);
-// 22 partial rounds; 4 x (RC, S-box, MDS).
+// 22 partial rounds; 4 x (RC, S-box, MDS).  OUT: the outputs the caller reads (the others are
+// left unspecified); the last full round is peeled so that its MDS forms only those.
+template <int OUT = OUT_ALL>
 __device__ __forceinline__ void permute(State& s) {
     uint64_t L[12], H[12], Z[12];
     mds_ext_limbs(s.lo, L);
@@ -197,8 +216,9 @@ __device__ __forceinline__ void permute(State& s) {
         H[i] = Z[i] >> 32;
     }
 #pragma unroll 1
-    for (int r = 26; r < 30; r++) full_round(s, L, H, r);
-    reduce12(L, H, s.lo, s.hi);
+    for (int r = 26; r < 29; r++) full_round(s, L, H, r);
+    full_round<OUT>(s, L, H, 29);
+    reduce12<OUT>(L, H, s.lo, s.hi);
 }
 
 __device__ __forceinline__ void permute(uint64_t v[12]) {

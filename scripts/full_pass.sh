@@ -1,6 +1,6 @@
-# Round-4 full GPU pass: smoke(), every GPU test, the bench at C1 / C2 / C5 / C4, and the N > 1
+# Full GPU pass: smoke(), every GPU test, the bench at C1 / C2 / C5 / C4, and the N > 1
 # launch paths (torchrun x2 and self-launched x4 over the gloo rehearsal transport, C2).
-# usage: bash scripts/r4_full.sh TAG
+# usage: bash scripts/full_pass.sh TAG
 set -u
 TAG=${1:-r4full}
 cd "$GRAFT_REPO_ROOT" && mkdir -p gpurun_out/$TAG && export TMPDIR=/tmp

@@ -1,4 +1,4 @@
-# usage: bash scripts/r4_check.sh TAG  -- LDE parity tests, a bench line and a kernel-trace summary
+# usage: bash scripts/lde_check.sh TAG  -- LDE parity tests, a bench line and a kernel-trace summary
 set -u
 TAG=$1
 cd "$GRAFT_REPO_ROOT" && mkdir -p gpurun_out/$TAG && export TMPDIR=/tmp

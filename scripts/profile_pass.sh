@@ -1,6 +1,6 @@
-# Round-4 evidence pass for the C3 bench: the default bench line (with the CPU baseline), a
+# Evidence pass for the C3 bench: the default bench line (with the CPU baseline), a
 # kernel-trace stats run, and one PMC pass per counter group (HBM fetch, HBM write, SQ issue).
-# usage: bash scripts/r4_profile.sh TAG
+# usage: bash scripts/profile_pass.sh TAG
 set -u
 TAG=${1:-r4}
 cd "$GRAFT_REPO_ROOT"

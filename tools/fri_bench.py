@@ -17,6 +17,7 @@ import sys
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, os.path.join(ROOT, "era-boojum_amd"))
+sys.path.insert(0, ROOT)
 
 HBM_PEAK_GBS = 8000.0
 VALU_PEAK_TSLOTS = 78.6432
@@ -55,7 +56,8 @@ def main():
     t_leaves = timed(torch, lambda: call("bj_merkle_leaves_chunked_d", c.data_ptr(), 2, n, nl, e, out.data_ptr(),
                                          stream_of(out)))
     census = json.load(open(os.path.join(ROOT, "era-boojum_amd", "boojum_amd", "valu_census.json")))
-    slots = census["issue_slots_per_perm"]
+    import bench
+    slots = bench.leaf_slots_per_perm(census, 2 * e)
     perms = nl * ((2 * e + 7) // 8)
     line = {
         "codeword": "GoldilocksExt2 x 2^%d (C3 FRI base oracle size)" % log_n,

@@ -1,5 +1,5 @@
 #!/usr/bin/env python3
-"""Per-launch HBM traffic and VALU counters from rocprofv3 PMC passes (scripts/profile_r1.sh).
+"""Per-launch HBM traffic and VALU counters from rocprofv3 PMC passes (scripts/profile_pass.sh).
 
 Reads <dir>/fetch, <dir>/write and <dir>/sq run_counter_collection.csv files, averages each
 counter per kernel over its dispatches and writes profiles/pmc_summary.json:

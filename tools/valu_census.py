@@ -2,10 +2,12 @@
 """Static VALU census of one Poseidon2 permutation as compiled for gfx950.
 
 The permutation (csrc/poseidon2.hpp) has three `#pragma unroll 1` round loops with fixed
-trip counts: 4 full rounds, 11 pairs of partial rounds and 4 full rounds. `node_level_kernel`
-(csrc/merkle.hip) runs exactly one permutation per lane, so its dynamic instruction
-stream is known statically:
-    straight-line code x1 + loop bodies x (4, 11, 4).
+trip counts: 4 full rounds, 11 pairs of partial rounds and 3 full rounds (the last full round
+is peeled, so that its MDS forms only the outputs the caller reads). The census kernels of
+tools/census_perm.hip run exactly one permutation per lane in each output form (all 12
+words, the capacity words, the digest), so their dynamic instruction stream is known
+statically:
+    straight-line code x1 + loop bodies x (4, 11, 3).
 This tool disassembles the gfx950 code object and weights each VALU instruction by the
 issue cost measured in profiles/r1_isa_rates.txt:
 * 1 slot: full-rate 32-bit ops (v_add_u32, v_mov_b32, logic);
@@ -32,8 +34,8 @@ FULL_RATE = re.compile(r"^v_(add_u32_e32|sub_u32_e32|mov_b32|and_b32_e32|or_b32_
                        r"lshrrev_b32_e32|not_b32|bitop3_b32)")
 
 
-def disassemble(name="merkle"):
-    src = os.path.join(ROOT, "era-boojum_amd", "csrc", name + ".hip")
+def disassemble(name="merkle", src=None):
+    src = src or os.path.join(ROOT, "era-boojum_amd", "csrc", name + ".hip")
     dev = "/tmp/_census_%s_dev.o" % name
     co = "/tmp/_census_%s.co" % name
     subprocess.run([HIPCC, "-O3", "-std=c++17", "--offload-arch=gfx950", "--cuda-device-only", "-c", "-o", dev,
@@ -72,7 +74,7 @@ def parse(lines):
     return instrs
 
 
-def census(instrs, trips=(4, 11, 4)):
+def census(instrs, trips=(4, 11, 3)):
     base = instrs[0][0]
     back = [(i, a, t) for i, (a, mn, t) in enumerate(instrs) if t is not None and base + t < a]
     if len(back) != len(trips):
@@ -192,12 +194,19 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--json")
     args = ap.parse_args()
-    dis = disassemble()
-    instrs = parse(kernel_lines(dis, "node_level_kernel"))
-    valu, slots, hist = census(instrs)
-    res = {"kernel": "node_level_kernel (one Poseidon2 permutation per lane + 64 B in / 32 B out)",
-           "valu_instr_per_perm": valu, "issue_slots_per_perm": slots,
-           "top": dict(sorted(hist.items(), key=lambda kv: -kv[1])[:12]),
+    # one permutation per lane in each output form (tools/census_perm.hip): the loads and stores
+    # around it are a few instructions of 10k
+    dis = disassemble("census_perm", os.path.join(ROOT, "tools", "census_perm.hip"))
+    forms = {}
+    for form in ("all", "cap", "digest"):
+        valu, slots, hist = census(parse(kernel_lines(dis, "census_perm_" + form)))
+        forms[form] = {"valu": valu, "slots": slots}
+        if form == "all":
+            top = dict(sorted(hist.items(), key=lambda kv: -kv[1])[:12])
+    res = {"kernel": "census_perm_{all,cap,digest} (tools/census_perm.hip: one Poseidon2 permutation per lane)",
+           "valu_instr_per_perm": forms["all"]["valu"], "issue_slots_per_perm": forms["all"]["slots"],
+           "perm_forms": forms,
+           "top": top,
            "ntt_ct": ntt_census(),
            "lde3": lde3_census(),
            "blake2s": blake2s_census()}
