@@ -11,7 +11,8 @@
  *      distribute_powers -- called concurrently from T threads on distinct columns, three rounds
  *      (an earlier null-stream version of the seam returned a stale column about every other run);
  *   2. TreeHasher leaf/node (cs/oracle/mod.rs:141-168);
- *   3. the whole witness commit through the host-buffer entry point bj_lde_commit_h
+ *   3. the whole witness commit through the host-buffer entry point bj_lde_commit_h, and
+ *      through the device-resident one-call bj_lde_commit_ex_d (flags 0) on hipMalloc buffers
  *      (prover.rs:313-353): LDE at D, tree over the first k cosets (subset_for_degree,
  *      prover.rs:325-347); LDE, leaves, nodes and cap bit-exact;
  *   4. the collective sharded commit (bj_sharded_commit_d) at G = 2, 4, 8 ranks as threads on
@@ -190,6 +191,28 @@ static void check_commit(uint32_t log_n, uint32_t n_cols, uint32_t log_lde, uint
     CHECK(eq_canon(leaves, r_leaves, 4 * nl, &w), "leaves differ at %zu", w);
     CHECK(eq_canon(nodes, r_nodes, 4 * n_nodes, &w), "nodes differ at %zu", w);
     CHECK(eq_canon(cap_out, r_cap, 4 * cap, &w), "cap differs at %zu", w);
+    /* the device-resident one-call commit (ABI 2.4, flags 0: no monomial write-back), HBM buffers
+     * from hipMalloc, the legacy stream: the mode a GPU-resident Rust prover uses */
+    u64 *d_tr = NULL, *d_scr = NULL, *d_lde = NULL, *d_lv = NULL, *d_nd = NULL;
+    u64 d_cap[4 * 4096];
+    int ok = hipMalloc((void**)&d_tr, 8 * n * n_cols) == hipSuccess && hipMalloc((void**)&d_scr, 8 * n * n_cols) == hipSuccess &&
+             hipMalloc((void**)&d_lde, 8 * nd * n_cols) == hipSuccess && hipMalloc((void**)&d_lv, 32 * nl) == hipSuccess &&
+             hipMalloc((void**)&d_nd, 32 * n_nodes) == hipSuccess &&
+             hipMemcpy(d_tr, trace, 8 * n * n_cols, hipMemcpyHostToDevice) == hipSuccess;
+    CHECK(ok, "device buffers for bj_lde_commit_ex_d");
+    if (ok) {
+        rc = bj_lde_commit_ex_d(d_tr, n_cols, n, log_n, log_lde, log_k, cap, d_scr, d_lde, d_lv, d_nd, d_cap, 0, NULL);
+        CHECK(rc == BJ_OK, "bj_lde_commit_ex_d: rc %d (%s)", rc, bj_last_error());
+        CHECK(hipMemcpy(lde, d_lde, 8 * nd * n_cols, hipMemcpyDeviceToHost) == hipSuccess &&
+                  hipMemcpy(leaves, d_lv, 32 * nl, hipMemcpyDeviceToHost) == hipSuccess &&
+                  hipMemcpy(nodes, d_nd, 32 * n_nodes, hipMemcpyDeviceToHost) == hipSuccess,
+              "copy back");
+        CHECK(eq_canon(lde, r_lde, nd * n_cols, &w), "device commit: LDE differs at %zu", w);
+        CHECK(eq_canon(leaves, r_leaves, 4 * nl, &w), "device commit: leaves differ at %zu", w);
+        CHECK(eq_canon(nodes, r_nodes, 4 * n_nodes, &w), "device commit: nodes differ at %zu", w);
+        CHECK(eq_canon(d_cap, r_cap, 4 * cap, &w), "device commit: cap differs at %zu", w);
+    }
+    hipFree(d_tr); hipFree(d_scr); hipFree(d_lde); hipFree(d_lv); hipFree(d_nd);
     free(trace); free(lde); free(leaves); free(nodes); free(r_lde); free(r_leaves); free(r_nodes);
 }
 
