@@ -604,36 +604,6 @@ int bj_monomials_to_lde_d(const uint64_t* monomials, uint32_t n_cols, size_t mon
     return lde_forward(lde, (size_t)D * n, n, 0, D, monomials, mono_stride, false, n_cols, log_n, log_lde, S(stream));
 }
 
-namespace {
-// A second stream of the calling thread per device, with a pool of fork / join events (created
-// once, grown on demand).  Work forked to it is always joined back to the caller's stream
-// before a call returns, so the call stays stream-ordered (and capturable in a graph).
-struct AuxStream {
-    hipStream_t s = nullptr, s2 = nullptr;
-    std::vector<hipEvent_t> ev;
-};
-int aux_stream(size_t n_events, AuxStream** out) {
-    thread_local std::map<int, AuxStream> tl;
-    int dev = 0;
-    HIP_TRY(hipGetDevice(&dev), "hipGetDevice");
-    AuxStream& a = tl[dev];
-    if (!a.s) HIP_TRY(hipStreamCreateWithFlags(&a.s, hipStreamNonBlocking), "hipStreamCreate");
-    if (!a.s2) HIP_TRY(hipStreamCreateWithFlags(&a.s2, hipStreamNonBlocking), "hipStreamCreate");
-    while (a.ev.size() < n_events) {
-        hipEvent_t e;
-        HIP_TRY(hipEventCreateWithFlags(&e, hipEventDisableTiming), "hipEventCreate");
-        a.ev.push_back(e);
-    }
-    *out = &a;
-    return BJ_OK;
-}
-
-uint32_t env_u32(const char* name, uint32_t dflt) {
-    const char* e = getenv(name);
-    return e ? (uint32_t)strtoul(e, nullptr, 0) : dflt;
-}
-}  // namespace
-
 int bj_lde_ex_d(const uint64_t* trace, uint32_t n_cols, size_t trace_stride, uint32_t log_n, uint32_t log_lde,
                 uint64_t* scratch, uint64_t* lde, uint32_t flags, void* stream) {
     if (flags & ~BJ_LDE_KEEP_MONOMIALS) return fail(BJ_EINVAL, "unknown bj_lde_ex_d flags");
@@ -653,49 +623,9 @@ int bj_lde_ex_d(const uint64_t* trace, uint32_t n_cols, size_t trace_stride, uin
         uint64_t* mono = (flags & BJ_LDE_KEEP_MONOMIALS) ? scratch : nullptr;
         const size_t L = bj::lde3_table_len(log_n);
         hipStream_t st = S(stream);
-        const uint32_t chunk = env_u32("BJ_LDE_OVERLAP", 0);
-        if (chunk == 0 || chunk >= n_cols) {
-            HIP_TRY(bj::launch_ct_inverse_head(scratch, n, trace, trace_stride, n_cols, log_n, inv, st), "ifft");
-            HIP_TRY(bj::launch_lde3(lde, (size_t)D * n, n, D, scratch, n, mono, n, n_cols, log_n, inv, tabs, L, st),
-                    "lde");
-            return BJ_OK;
-        }
-        // column chunks: the middle pass of chunk k on the caller's stream, its final pass on the
-        // second stream once chunk k's middle pass is done, so the (latency-bound, VALU-heavy)
-        // middle pass of chunk k + 1 shares the CUs with the (HBM-heavy) final pass of chunk k;
-        // BJ_LDE_OVERLAP_HEAD=1: the inverse head by chunk too, on a third stream, ahead
-        const bool head_chunks = env_u32("BJ_LDE_OVERLAP_HEAD", 0) != 0;
-        const uint32_t K = (n_cols + chunk - 1) / chunk;
-        AuxStream* ax;
-        if (int r = aux_stream(2 * K + 2, &ax)) return r;
-        if (!head_chunks)
-            HIP_TRY(bj::launch_ct_inverse_head(scratch, n, trace, trace_stride, n_cols, log_n, inv, st), "ifft");
-        else {
-            HIP_TRY(hipEventRecord(ax->ev[2 * K + 1], st), "hipEventRecord");
-            HIP_TRY(hipStreamWaitEvent(ax->s2, ax->ev[2 * K + 1], 0), "hipStreamWaitEvent");
-        }
-        for (uint32_t k = 0; k < K; k++) {
-            const uint32_t c0 = k * chunk, cc = std::min(chunk, n_cols - c0);
-            uint64_t* l = lde + (size_t)c0 * D * n;
-            if (head_chunks) {
-                HIP_TRY(bj::launch_ct_inverse_head(scratch + (size_t)c0 * n, n, trace + (size_t)c0 * trace_stride,
-                                                   trace_stride, cc, log_n, inv, ax->s2),
-                        "ifft");
-                HIP_TRY(hipEventRecord(ax->ev[K + 1 + k], ax->s2), "hipEventRecord");
-                HIP_TRY(hipStreamWaitEvent(st, ax->ev[K + 1 + k], 0), "hipStreamWaitEvent");
-            }
-            HIP_TRY(bj::launch_lde3(l, (size_t)D * n, n, D, scratch + (size_t)c0 * n, n,
-                                    mono ? mono + (size_t)c0 * n : nullptr, n, cc, log_n, inv, tabs, L, st, 31, 0,
-                                    bj::LDE3_MID),
-                    "lde");
-            HIP_TRY(hipEventRecord(ax->ev[k], st), "hipEventRecord");
-            HIP_TRY(hipStreamWaitEvent(ax->s, ax->ev[k], 0), "hipStreamWaitEvent");
-            HIP_TRY(bj::launch_lde3(l, (size_t)D * n, n, D, nullptr, 0, nullptr, 0, cc, log_n, nullptr, tabs, L, ax->s,
-                                    31, 0, bj::LDE3_FINAL),
-                    "lde");
-        }
-        HIP_TRY(hipEventRecord(ax->ev[K], ax->s), "hipEventRecord");
-        HIP_TRY(hipStreamWaitEvent(st, ax->ev[K], 0), "hipStreamWaitEvent");
+        HIP_TRY(bj::launch_ct_inverse_head(scratch, n, trace, trace_stride, n_cols, log_n, inv, st), "ifft");
+        HIP_TRY(bj::launch_lde3(lde, (size_t)D * n, n, D, scratch, n, mono, n, n_cols, log_n, inv, tabs, L, st),
+                "lde");
         return BJ_OK;
     }
     // iFFT (utils.rs:295-304): scratch = monomials in bit-reversed order; the forward pass
