@@ -181,6 +181,11 @@ static void check_commit(uint32_t log_n, uint32_t n_cols, uint32_t log_lde, uint
     for (uint32_t c = 0; c < n_cols; c++)
         for (size_t r = 0; r < n; r++) trace[(size_t)c * n + r] = canon(splitmix64(42 + (u64)c * n + r));
     u64* lde = xmalloc(8 * nd * n_cols), *leaves = xmalloc(32 * nl), *nodes = xmalloc(32 * n_nodes);
+    /* the trace into HBM for the device-resident call below, now: the oracle transforms its
+     * input in place */
+    u64 *d_tr = NULL, *d_scr = NULL, *d_lde = NULL, *d_lv = NULL, *d_nd = NULL;
+    int ok = hipMalloc((void**)&d_tr, 8 * n * n_cols) == hipSuccess &&
+             hipMemcpy(d_tr, trace, 8 * n * n_cols, hipMemcpyHostToDevice) == hipSuccess;
     int rc = bj_lde_commit_h(trace, n_cols, log_n, log_lde, log_k, cap, lde, leaves, nodes, cap_out);
     CHECK(rc == BJ_OK, "bj_lde_commit_h: rc %d (%s)", rc, bj_last_error());
     u64* r_lde = xmalloc(8 * nd * n_cols), *r_leaves = xmalloc(32 * nl), *r_nodes = xmalloc(32 * n_nodes);
@@ -193,12 +198,10 @@ static void check_commit(uint32_t log_n, uint32_t n_cols, uint32_t log_lde, uint
     CHECK(eq_canon(cap_out, r_cap, 4 * cap, &w), "cap differs at %zu", w);
     /* the device-resident one-call commit (ABI 2.4, flags 0: no monomial write-back), HBM buffers
      * from hipMalloc, the legacy stream: the mode a GPU-resident Rust prover uses */
-    u64 *d_tr = NULL, *d_scr = NULL, *d_lde = NULL, *d_lv = NULL, *d_nd = NULL;
     u64 d_cap[4 * 4096];
-    int ok = hipMalloc((void**)&d_tr, 8 * n * n_cols) == hipSuccess && hipMalloc((void**)&d_scr, 8 * n * n_cols) == hipSuccess &&
-             hipMalloc((void**)&d_lde, 8 * nd * n_cols) == hipSuccess && hipMalloc((void**)&d_lv, 32 * nl) == hipSuccess &&
-             hipMalloc((void**)&d_nd, 32 * n_nodes) == hipSuccess &&
-             hipMemcpy(d_tr, trace, 8 * n * n_cols, hipMemcpyHostToDevice) == hipSuccess;
+    ok = ok && hipMalloc((void**)&d_scr, 8 * n * n_cols) == hipSuccess &&
+         hipMalloc((void**)&d_lde, 8 * nd * n_cols) == hipSuccess && hipMalloc((void**)&d_lv, 32 * nl) == hipSuccess &&
+         hipMalloc((void**)&d_nd, 32 * n_nodes) == hipSuccess;
     CHECK(ok, "device buffers for bj_lde_commit_ex_d");
     if (ok) {
         rc = bj_lde_commit_ex_d(d_tr, n_cols, n, log_n, log_lde, log_k, cap, d_scr, d_lde, d_lv, d_nd, d_cap, 0, NULL);
