@@ -170,6 +170,44 @@ __device__ __forceinline__ size_t coset_offset(uint32_t i, size_t coset_stride, 
     return (size_t)(i >> log_k) * block_stride + (size_t)(i & ((1u << log_k) - 1)) * coset_stride;
 }
 
+// The inverse tail (ct_tail_kernel<., true>) on the registers of block q: local stages 0..12 of
+// the block (the inverse's stages R..R+12), n^-1 in TA.  In: x[k] = the inverse head's output at
+// block position t + 256 k; out: x[k] = c_j at block position l = 32 t + k, that is
+// j = bitrev_13(l) 2^R + bitrev_R(q) (the monomials in bit-reversed order, any u64 representative).
+template <int R>
+__device__ __forceinline__ void inverse_tail13(uint64_t* x, const uint64_t* __restrict__ inv_tab, uint32_t q,
+                                               uint32_t t, uint64_t* lds) {
+    constexpr uint32_t LOGN = R + 13;
+    const uint32_t ba = tail_base_a(t), bc = tail_base_c(t);
+    const uint64_t* ext = inv_tab + ((size_t)1 << LOGN);
+    uint64_t f[PT], wa[16], wb[16], wc[16];
+    load32(f, ext + EXT_TA + (size_t)q * 32);
+    prescale32(x, f);
+    dft_p2<5, true, 0>(x);
+    const uint32_t tlo = t & 7, thi = t >> 3;
+    const uint32_t bb = tail_base_b(thi, tlo);
+#pragma unroll
+    for (int k = 0; k < PT; k++) lds[ba + tail_off_a(k)] = x[k];
+    load32(f, ext + ext_tb(R) + ((((size_t)q << 5) | thi) << 5));
+    __syncthreads();
+#pragma unroll
+    for (int k = 0; k < PT; k++) x[k] = lds[bb + tail_off_b(k)];
+    prescale32(x, f);
+    dft_p2<5, true, 0>(x);
+    tw_ct_tailC<10>(wa, inv_tab, R, q, t);
+    // same slots as the reads just made by this thread: no barrier needed before the writes
+#pragma unroll
+    for (int k = 0; k < PT; k++) lds[bb + tail_off_b(k)] = x[k];
+    tw_ct_tailC<11>(wb, inv_tab, R, q, t);
+    tw_ct_tailC<12>(wc, inv_tab, R, q, t);
+    __syncthreads();
+#pragma unroll
+    for (int k = 0; k < PT; k++) x[k] = lds[bc + k];
+    ct_stage<4>(x, wa);
+    ct_stage<2>(x, wb);
+    ct_stage<1>(x, wc);
+}
+
 // ------------------------------------------------------------------ middle pass
 //
 // LDS layouts of the forward exchanges (element m = position within the block after the
@@ -206,34 +244,7 @@ __global__ __launch_bounds__(NT, 2) void lde3_mid_kernel(const uint64_t* src, si
             x[k] = from_u32x2(__builtin_amdgcn_raw_buffer_load_b64(rb, (int)(t * 8), k * 2048, 0));
     }
     if constexpr (INV_PART) {
-        // the inverse tail (ct_tail_kernel<., true>): local stages 0..12 of block q, n^-1 in TA
-        const uint64_t* ext = inv_tab + ((size_t)1 << LOGN);
-        uint64_t f[PT], wa[16], wb[16], wc[16];
-        load32(f, ext + EXT_TA + (size_t)q * 32);
-        prescale32(x, f);
-        dft_p2<5, true, 0>(x);
-        const uint32_t tlo = t & 7, thi = t >> 3;
-        const uint32_t bb = tail_base_b(thi, tlo);
-#pragma unroll
-        for (int k = 0; k < PT; k++) lds[ba + tail_off_a(k)] = x[k];
-        load32(f, ext + ext_tb(R) + ((((size_t)q << 5) | thi) << 5));
-        __syncthreads();
-#pragma unroll
-        for (int k = 0; k < PT; k++) x[k] = lds[bb + tail_off_b(k)];
-        prescale32(x, f);
-        dft_p2<5, true, 0>(x);
-        tw_ct_tailC<10>(wa, inv_tab, R, q, t);
-        // same slots as the reads just made by this thread: no barrier needed before the writes
-#pragma unroll
-        for (int k = 0; k < PT; k++) lds[bb + tail_off_b(k)] = x[k];
-        tw_ct_tailC<11>(wb, inv_tab, R, q, t);
-        tw_ct_tailC<12>(wc, inv_tab, R, q, t);
-        __syncthreads();
-#pragma unroll
-        for (int k = 0; k < PT; k++) x[k] = lds[bc + k];
-        ct_stage<4>(x, wa);
-        ct_stage<2>(x, wb);
-        ct_stage<1>(x, wc);
+        inverse_tail13<R>(x, inv_tab, q, t, lds);
     } else {
         // monomials already in bit-reversed order: re-deal the coalesced load to l = 32 t + k
 #pragma unroll
@@ -492,6 +503,71 @@ __global__ __launch_bounds__(NT, 2) void lde3_final_kernel(uint64_t* lde, size_t
     for (int k = 0; k < PT; k++) __builtin_amdgcn_raw_buffer_store_b64(as_u32x2(y[k]), rd, (int)(t * 8), k * 2048, 0);
 }
 
+// -------------------------------------------------- inverse tail + sub-coset fold (G > D)
+//
+// The sender side of the collective commit's G > D exchange when each rank's share is half a
+// coset (F = n / m = 2: collective.hip, shard.hip's fold_all_kernel): the monomials of block q
+// come out of the inverse tail with c_t and c_{t+m} in registers 2i, 2i + 1 (the top bit of j is
+// the bit 0 of l = 32 t + k), so each destination d's folded coefficient
+// h_u = c_t + (s_d^m) c_{t+m}, u = bitrev_m(t) = q 4096 + 16 t + i, is formed right there: the
+// monomials never reach memory and the separate fold pass (read n, write G m per column) goes.
+struct FoldZ {
+    uint64_t z[64];
+};
+
+typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
+
+template <int R>
+__global__ __launch_bounds__(NT, 2) void lde3_inv_fold2_kernel(const uint64_t* src, size_t src_stride, uint64_t* dst,
+                                                               size_t dst_col_stride, size_t dst_shard_stride,
+                                                               uint32_t n_cols, uint32_t shards,
+                                                               const uint64_t* __restrict__ inv_tab, FoldZ zc) {
+    __shared__ uint64_t lds[PAD_LDS];
+    const uint32_t t = threadIdx.x;
+    const uint32_t c = __builtin_amdgcn_readfirstlane(blockIdx.x % n_cols);
+    const uint32_t q = __builtin_amdgcn_readfirstlane(blockIdx.x / n_cols);
+    uint64_t x[PT];
+    {
+        const auto rb = uniform_rsrc(src + (size_t)c * src_stride + (size_t)q * TILE, 8u * TILE);
+#pragma unroll
+        for (int k = 0; k < PT; k++)
+            x[k] = from_u32x2(__builtin_amdgcn_raw_buffer_load_b64(rb, (int)(t * 8), k * 2048, 0));
+    }
+    inverse_tail13<R>(x, inv_tab, q, t, lds);
+#pragma unroll 1
+    for (uint32_t d = 0; d < shards; d++) {
+        const uint64_t z = zc.z[d];
+        const uint32_t z0 = __builtin_amdgcn_readfirstlane((uint32_t)z), z1 = __builtin_amdgcn_readfirstlane((uint32_t)(z >> 32));
+        uint64_t h[16];
+#pragma unroll
+        for (int i = 0; i < 16; i += 4) {
+            uint32_t p0[4], p1[4], s0[4], s1[4];
+            glasm::mul_sb_x4((uint32_t)x[2 * i + 1], (uint32_t)(x[2 * i + 1] >> 32), z0, z1, p0[0], p1[0],
+                             (uint32_t)x[2 * i + 3], (uint32_t)(x[2 * i + 3] >> 32), z0, z1, p0[1], p1[1],
+                             (uint32_t)x[2 * i + 5], (uint32_t)(x[2 * i + 5] >> 32), z0, z1, p0[2], p1[2],
+                             (uint32_t)x[2 * i + 7], (uint32_t)(x[2 * i + 7] >> 32), z0, z1, p0[3], p1[3]);
+            glasm::add_x4((uint32_t)x[2 * i], (uint32_t)(x[2 * i] >> 32), p0[0], p1[0], s0[0], s1[0],
+                          (uint32_t)x[2 * i + 2], (uint32_t)(x[2 * i + 2] >> 32), p0[1], p1[1], s0[1], s1[1],
+                          (uint32_t)x[2 * i + 4], (uint32_t)(x[2 * i + 4] >> 32), p0[2], p1[2], s0[2], s1[2],
+                          (uint32_t)x[2 * i + 6], (uint32_t)(x[2 * i + 6] >> 32), p0[3], p1[3], s0[3], s1[3]);
+#pragma unroll
+            for (int e = 0; e < 4; e++) h[i + e] = join2(s0[e], s1[e]);
+        }
+        // 16 consecutive words per thread: 16-byte stores, the wave's 8 KiB contiguous
+        const auto rd = uniform_rsrc(dst + (size_t)d * dst_shard_stride + (size_t)c * dst_col_stride + (size_t)q * 4096,
+                                     8u * 4096);
+#pragma unroll
+        for (int i = 0; i < 8; i++) {
+            u32x4 v;
+            v.x = (uint32_t)h[2 * i];
+            v.y = (uint32_t)(h[2 * i] >> 32);
+            v.z = (uint32_t)h[2 * i + 1];
+            v.w = (uint32_t)(h[2 * i + 1] >> 32);
+            __builtin_amdgcn_raw_buffer_store_b128(v, rd, (int)(t * 128 + i * 16), 0, 0);
+        }
+    }
+}
+
 // ------------------------------------------------------------------- table
 __global__ void lde3_table_kernel(uint64_t* out, uint32_t log_n, uint64_t w_n, uint64_t s, size_t len) {
     const size_t n = (size_t)1 << log_n;
@@ -596,6 +672,26 @@ hipError_t launch_lde3(uint64_t* lde, size_t col_stride, size_t coset_stride, ui
         default: BJ_LDE3(10); break;
     }
 #undef BJ_LDE3
+    return hipGetLastError();
+}
+
+hipError_t launch_lde3_inverse_fold2(uint64_t* dst, size_t dst_col_stride, size_t dst_shard_stride,
+                                     const uint64_t* src, size_t src_stride, uint32_t n_cols, uint32_t log_n,
+                                     const uint64_t* inv_tab, const uint64_t* z, uint32_t shards, hipStream_t st) {
+    if (n_cols == 0 || shards == 0) return hipSuccess;
+    if (!lde3_supported(log_n) || shards > 64) return hipErrorInvalidValue;
+    FoldZ zc;
+    for (uint32_t d = 0; d < 64; d++) zc.z[d] = d < shards ? z[d] : 0;
+    const uint32_t R = log_n - 13;
+    const dim3 g(n_cols << R);
+    switch (R) {
+        case 5: hipLaunchKernelGGL(lde3_inv_fold2_kernel<5>, g, dim3(NT), 0, st, src, src_stride, dst, dst_col_stride, dst_shard_stride, n_cols, shards, inv_tab, zc); break;
+        case 6: hipLaunchKernelGGL(lde3_inv_fold2_kernel<6>, g, dim3(NT), 0, st, src, src_stride, dst, dst_col_stride, dst_shard_stride, n_cols, shards, inv_tab, zc); break;
+        case 7: hipLaunchKernelGGL(lde3_inv_fold2_kernel<7>, g, dim3(NT), 0, st, src, src_stride, dst, dst_col_stride, dst_shard_stride, n_cols, shards, inv_tab, zc); break;
+        case 8: hipLaunchKernelGGL(lde3_inv_fold2_kernel<8>, g, dim3(NT), 0, st, src, src_stride, dst, dst_col_stride, dst_shard_stride, n_cols, shards, inv_tab, zc); break;
+        case 9: hipLaunchKernelGGL(lde3_inv_fold2_kernel<9>, g, dim3(NT), 0, st, src, src_stride, dst, dst_col_stride, dst_shard_stride, n_cols, shards, inv_tab, zc); break;
+        default: hipLaunchKernelGGL(lde3_inv_fold2_kernel<10>, g, dim3(NT), 0, st, src, src_stride, dst, dst_col_stride, dst_shard_stride, n_cols, shards, inv_tab, zc); break;
+    }
     return hipGetLastError();
 }
 
