@@ -40,13 +40,6 @@ hipError_t launch_lde_forward(uint64_t* lde, size_t lde_col_stride, uint32_t n_c
 // power table sizes for a column of 2^log_n: lo 4096, hi max(1, n / 4096)
 inline size_t pw_hi_len(uint32_t log_n) { return log_n > 12 ? ((size_t)1 << (log_n - 12)) : 1; }
 
-// The inverse tail of the three-pass form fused with the G > D sub-coset fold at F = 2
-// (ntt_lde3.hip): src = the inverse head's output (n_cols columns of 2^log_n at src_stride);
-// for each destination d < shards (<= 64), column c: the m = n / 2 folded coefficients
-// h = c_t + z[d] c_{t+m} in bit-reversed order at dst + d * dst_shard_stride + c * dst_col_stride.
-hipError_t launch_lde3_inverse_fold2(uint64_t* dst, size_t dst_col_stride, size_t dst_shard_stride,
-                                     const uint64_t* src, size_t src_stride, uint32_t n_cols, uint32_t log_n,
-                                     const uint64_t* inv_tab, const uint64_t* z, uint32_t shards, hipStream_t st);
 }  // namespace bj
 
 namespace bj {
@@ -136,11 +129,6 @@ uint64_t shard_shift(uint32_t log_n, uint32_t log_lde, uint32_t log_shards, uint
 // lde + (i >> log_k) * block_stride + c * col_stride + (i mod 2^log_k) * 2^log_n.  scratch holds
 // n_cols * 2^log_n words.  False (nothing launched) when log_n is outside the three-pass range.
 bool lde_fused_supported(uint32_t log_n);
-// capi.hip: the inverse head and launch_lde3_inverse_fold2 (the G > D exchange's sender side
-// at F = 2), scratch n_cols * 2^log_n words.  False (nothing launched) outside 2^18..2^23.
-int inverse_fold2(const uint64_t* trace, uint32_t n_cols, size_t trace_stride, uint32_t log_n, uint64_t* scratch,
-                  uint64_t* dst, size_t dst_col_stride, size_t dst_shard_stride, const uint64_t* z, uint32_t shards,
-                  hipStream_t st);
 int lde_fused_blocks(const uint64_t* trace, uint32_t n_cols, size_t trace_stride, uint32_t log_n, uint32_t log_lde,
                      uint32_t log_k, uint64_t* scratch, uint64_t* lde, size_t col_stride, size_t block_stride,
                      hipStream_t st);

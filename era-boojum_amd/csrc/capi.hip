@@ -396,21 +396,6 @@ int lde_fused_blocks(const uint64_t* trace, uint32_t n_cols, size_t trace_stride
     return BJ_OK;
 }
 
-int inverse_fold2(const uint64_t* trace, uint32_t n_cols, size_t trace_stride, uint32_t log_n, uint64_t* scratch,
-                  uint64_t* dst, size_t dst_col_stride, size_t dst_shard_stride, const uint64_t* z, uint32_t shards,
-                  hipStream_t st) {
-    if (!use_lde3(log_n)) return fail(BJ_EINVAL, "internal: fused inverse + fold outside 2^18..2^23");
-    if (n_cols == 0) return BJ_OK;
-    const uint64_t* inv;
-    if (int r = get_ct(log_n, true, 1, &inv)) return r;
-    HIP_TRY(bj::launch_ct_inverse_head(scratch, (size_t)1 << log_n, trace, trace_stride, n_cols, log_n, inv, st),
-            "ifft");
-    HIP_TRY(bj::launch_lde3_inverse_fold2(dst, dst_col_stride, dst_shard_stride, scratch, (size_t)1 << log_n, n_cols,
-                                          log_n, inv, z, shards, st),
-            "fold");
-    return BJ_OK;
-}
-
 uint64_t shard_shift(uint32_t log_n, uint32_t log_lde, uint32_t log_shards, uint32_t shard) {
     return ::shard_shift(log_n, log_lde, log_shards, shard);
 }

@@ -649,14 +649,6 @@ int bj_sharded_commit_d(bj_comm* comm, const uint64_t* trace_shard, size_t trace
         HIP_CHECK(arrived.make(K), "hipEventCreate");
     }
     std::vector<uint64_t> spm(world);
-    // G = 2 D / k (half a coset per rank) in the three-pass range: the fold rides on the inverse
-    // tail (ntt_lde3.hip lde3_inv_fold2_kernel); BJ_FUSED_FOLD=0 keeps the separate fold pass
-    const char* ff = getenv("BJ_FUSED_FOLD");
-    const bool fused_fold = fold && log_f == 1 && bj::lde_fused_supported(log_n) && (size_t)B * world <= 64 &&
-                            !(ff && ff[0] == '0');
-    std::vector<uint64_t> zall;
-    if (fused_fold)
-        for (uint32_t d = 0; d < B * world; d++) zall.push_back(gl::pow(bj::shard_shift(log_n, log_lde, ls, d), m));
     // phases 0 inverse (+ fold), 1 lde, 2 leaves, 3 nodes (bj_comm_set_timing)
     if (!comm->intervals.empty()) fold_intervals(comm, false);
     PhaseTimer pt(comm, st);
@@ -672,19 +664,13 @@ int bj_sharded_commit_d(bj_comm* comm, const uint64_t* trace_shard, size_t trace
             uint64_t* snd = send + (size_t)world * B * m * r.lo;
             uint64_t* mine = own + (size_t)r.lo * n;
             BJ_CHECK(pt.begin(0));
-            if (fused_fold) {
-                // half a coset per rank: the inverse tail folds for every (block, rank) in registers
-                BJ_CHECK(bj::inverse_fold2(tr, r.count, trace_stride, log_n, mine, snd, m, (size_t)r.count * m,
-                                           zall.data(), B * world, st));
-            } else {
-                BJ_CHECK(bj_lde_coeffs_d(tr, r.count, trace_stride, log_n, mine, n, st));
-                for (uint32_t j = 0; j < B; j++) {
-                    for (uint32_t p = 0; p < world; p++)
-                        spm[p] = gl::pow(bj::shard_shift(log_n, log_lde, ls, j * world + p), m);
-                    HIP_CHECK(bj::launch_fold_all(snd + (size_t)j * world * r.count * m, m, (size_t)r.count * m, mine,
-                                                  n, r.count, log2u(m), log_f, world, spm.data(), st),
-                              "fold");
-                }
+            BJ_CHECK(bj_lde_coeffs_d(tr, r.count, trace_stride, log_n, mine, n, st));
+            for (uint32_t j = 0; j < B; j++) {
+                for (uint32_t p = 0; p < world; p++)
+                    spm[p] = gl::pow(bj::shard_shift(log_n, log_lde, ls, j * world + p), m);
+                HIP_CHECK(bj::launch_fold_all(snd + (size_t)j * world * r.count * m, m, (size_t)r.count * m, mine, n,
+                                              r.count, log2u(m), log_f, world, spm.data(), st),
+                          "fold");
             }
             BJ_CHECK(pt.end());
             if (world > 1) {

@@ -503,71 +503,6 @@ __global__ __launch_bounds__(NT, 2) void lde3_final_kernel(uint64_t* lde, size_t
     for (int k = 0; k < PT; k++) __builtin_amdgcn_raw_buffer_store_b64(as_u32x2(y[k]), rd, (int)(t * 8), k * 2048, 0);
 }
 
-// -------------------------------------------------- inverse tail + sub-coset fold (G > D)
-//
-// The sender side of the collective commit's G > D exchange when each rank's share is half a
-// coset (F = n / m = 2: collective.hip, shard.hip's fold_all_kernel): the monomials of block q
-// come out of the inverse tail with c_t and c_{t+m} in registers 2i, 2i + 1 (the top bit of j is
-// the bit 0 of l = 32 t + k), so each destination d's folded coefficient
-// h_u = c_t + (s_d^m) c_{t+m}, u = bitrev_m(t) = q 4096 + 16 t + i, is formed right there: the
-// monomials never reach memory and the separate fold pass (read n, write G m per column) goes.
-struct FoldZ {
-    uint64_t z[64];
-};
-
-typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
-
-template <int R>
-__global__ __launch_bounds__(NT, 2) void lde3_inv_fold2_kernel(const uint64_t* src, size_t src_stride, uint64_t* dst,
-                                                               size_t dst_col_stride, size_t dst_shard_stride,
-                                                               uint32_t n_cols, uint32_t shards,
-                                                               const uint64_t* __restrict__ inv_tab, FoldZ zc) {
-    __shared__ uint64_t lds[PAD_LDS];
-    const uint32_t t = threadIdx.x;
-    const uint32_t c = __builtin_amdgcn_readfirstlane(blockIdx.x % n_cols);
-    const uint32_t q = __builtin_amdgcn_readfirstlane(blockIdx.x / n_cols);
-    uint64_t x[PT];
-    {
-        const auto rb = uniform_rsrc(src + (size_t)c * src_stride + (size_t)q * TILE, 8u * TILE);
-#pragma unroll
-        for (int k = 0; k < PT; k++)
-            x[k] = from_u32x2(__builtin_amdgcn_raw_buffer_load_b64(rb, (int)(t * 8), k * 2048, 0));
-    }
-    inverse_tail13<R>(x, inv_tab, q, t, lds);
-#pragma unroll 1
-    for (uint32_t d = 0; d < shards; d++) {
-        const uint64_t z = zc.z[d];
-        const uint32_t z0 = __builtin_amdgcn_readfirstlane((uint32_t)z), z1 = __builtin_amdgcn_readfirstlane((uint32_t)(z >> 32));
-        uint64_t h[16];
-#pragma unroll
-        for (int i = 0; i < 16; i += 4) {
-            uint32_t p0[4], p1[4], s0[4], s1[4];
-            glasm::mul_sb_x4((uint32_t)x[2 * i + 1], (uint32_t)(x[2 * i + 1] >> 32), z0, z1, p0[0], p1[0],
-                             (uint32_t)x[2 * i + 3], (uint32_t)(x[2 * i + 3] >> 32), z0, z1, p0[1], p1[1],
-                             (uint32_t)x[2 * i + 5], (uint32_t)(x[2 * i + 5] >> 32), z0, z1, p0[2], p1[2],
-                             (uint32_t)x[2 * i + 7], (uint32_t)(x[2 * i + 7] >> 32), z0, z1, p0[3], p1[3]);
-            glasm::add_x4((uint32_t)x[2 * i], (uint32_t)(x[2 * i] >> 32), p0[0], p1[0], s0[0], s1[0],
-                          (uint32_t)x[2 * i + 2], (uint32_t)(x[2 * i + 2] >> 32), p0[1], p1[1], s0[1], s1[1],
-                          (uint32_t)x[2 * i + 4], (uint32_t)(x[2 * i + 4] >> 32), p0[2], p1[2], s0[2], s1[2],
-                          (uint32_t)x[2 * i + 6], (uint32_t)(x[2 * i + 6] >> 32), p0[3], p1[3], s0[3], s1[3]);
-#pragma unroll
-            for (int e = 0; e < 4; e++) h[i + e] = join2(s0[e], s1[e]);
-        }
-        // 16 consecutive words per thread: 16-byte stores, the wave's 8 KiB contiguous
-        const auto rd = uniform_rsrc(dst + (size_t)d * dst_shard_stride + (size_t)c * dst_col_stride + (size_t)q * 4096,
-                                     8u * 4096);
-#pragma unroll
-        for (int i = 0; i < 8; i++) {
-            u32x4 v;
-            v.x = (uint32_t)h[2 * i];
-            v.y = (uint32_t)(h[2 * i] >> 32);
-            v.z = (uint32_t)h[2 * i + 1];
-            v.w = (uint32_t)(h[2 * i + 1] >> 32);
-            __builtin_amdgcn_raw_buffer_store_b128(v, rd, (int)(t * 128 + i * 16), 0, 0);
-        }
-    }
-}
-
 // ------------------------------------------------------------------- table
 __global__ void lde3_table_kernel(uint64_t* out, uint32_t log_n, uint64_t w_n, uint64_t s, size_t len) {
     const size_t n = (size_t)1 << log_n;
@@ -672,26 +607,6 @@ hipError_t launch_lde3(uint64_t* lde, size_t col_stride, size_t coset_stride, ui
         default: BJ_LDE3(10); break;
     }
 #undef BJ_LDE3
-    return hipGetLastError();
-}
-
-hipError_t launch_lde3_inverse_fold2(uint64_t* dst, size_t dst_col_stride, size_t dst_shard_stride,
-                                     const uint64_t* src, size_t src_stride, uint32_t n_cols, uint32_t log_n,
-                                     const uint64_t* inv_tab, const uint64_t* z, uint32_t shards, hipStream_t st) {
-    if (n_cols == 0 || shards == 0) return hipSuccess;
-    if (!lde3_supported(log_n) || shards > 64) return hipErrorInvalidValue;
-    FoldZ zc;
-    for (uint32_t d = 0; d < 64; d++) zc.z[d] = d < shards ? z[d] : 0;
-    const uint32_t R = log_n - 13;
-    const dim3 g(n_cols << R);
-    switch (R) {
-        case 5: hipLaunchKernelGGL(lde3_inv_fold2_kernel<5>, g, dim3(NT), 0, st, src, src_stride, dst, dst_col_stride, dst_shard_stride, n_cols, shards, inv_tab, zc); break;
-        case 6: hipLaunchKernelGGL(lde3_inv_fold2_kernel<6>, g, dim3(NT), 0, st, src, src_stride, dst, dst_col_stride, dst_shard_stride, n_cols, shards, inv_tab, zc); break;
-        case 7: hipLaunchKernelGGL(lde3_inv_fold2_kernel<7>, g, dim3(NT), 0, st, src, src_stride, dst, dst_col_stride, dst_shard_stride, n_cols, shards, inv_tab, zc); break;
-        case 8: hipLaunchKernelGGL(lde3_inv_fold2_kernel<8>, g, dim3(NT), 0, st, src, src_stride, dst, dst_col_stride, dst_shard_stride, n_cols, shards, inv_tab, zc); break;
-        case 9: hipLaunchKernelGGL(lde3_inv_fold2_kernel<9>, g, dim3(NT), 0, st, src, src_stride, dst, dst_col_stride, dst_shard_stride, n_cols, shards, inv_tab, zc); break;
-        default: hipLaunchKernelGGL(lde3_inv_fold2_kernel<10>, g, dim3(NT), 0, st, src, src_stride, dst, dst_col_stride, dst_shard_stride, n_cols, shards, inv_tab, zc); break;
-    }
     return hipGetLastError();
 }
 

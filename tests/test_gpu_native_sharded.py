@@ -151,8 +151,7 @@ def run_local(torch, world, n_cols, log_n, log_lde, cap, hasher, log_k=None):
     (1, (16, 18, 2, 16, "poseidon2")),
     (1, (16, 18, 3, 32, "poseidon2", 1)),
     (1, (8, 19, 2, 16, "blake2s", 0)),
-    # G = 2 D in the three-pass range: the sender's fold rides on the inverse tail
-    # (lde3_inv_fold2_kernel), half a coset per rank
+    # G = 2 D in the three-pass range: half a coset per rank, the sender's fold
     (8, (16, 18, 2, 16, "poseidon2")),
     (8, (8, 19, 2, 4, "blake2s")),
 ])
@@ -163,22 +162,6 @@ def test_native_sharded_commit_local_ranks(torch_mod, world, cfg):
     ref = reference(n_cols, log_n, log_lde, cap, hasher, log_k)
     for P in range(world):
         check_rank(ref, P, world, cap, *outs[P], hasher=hasher)
-
-
-def test_fused_fold_equals_separate_fold(torch_mod):
-    """G = 2 D at 2^18: the fused inverse-tail fold (default) and the separate inverse + fold
-    passes (BJ_FUSED_FOLD=0) give every rank the same LDE slice, leaves, subtree and cap."""
-    import os
-    args = (torch_mod, 8, 16, 18, 2, 16, "poseidon2")
-    fused = run_local(*args)
-    os.environ["BJ_FUSED_FOLD"] = "0"
-    try:
-        plain = run_local(*args)
-    finally:
-        del os.environ["BJ_FUSED_FOLD"]
-    for P in range(8):
-        for a, b in zip(fused[P][:4], plain[P][:4]):
-            assert np.array_equal(a, b), "rank %d differs" % P
 
 
 def test_native_sharded_commit_rccl_world1(torch_mod):
