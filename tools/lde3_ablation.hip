@@ -166,13 +166,13 @@ int main() {
     const char* names[] = {"copy of production", "no F1 loads", "no F2 loads", "no F1/F2 loads", "no data load",
                            "no store", "F2 as A*U (16 + 32 small-table loads, 32 extra products)"};
     float ms = time_ms([&] {
-        hipLaunchKernelGGL((lde3_final_kernel<9, 1>), gf, dim3(NT), 0, 0, lde, n * cosets, n, cols, cosets,
-                           (const uint64_t*)tabs, L);
+        hipLaunchKernelGGL((lde3_final_kernel<9, 1>), gf, dim3(NT), 0, 0, lde, n * cosets, n, (size_t)0, 31u, cols,
+                           cosets, (const uint64_t*)tabs, L);
     });
     printf("{\"kernel\": \"final\", \"variant\": \"production (F1 in LDS, phase 2 = A U from LDS)\", \"ms\": %.3f}\n", ms);
     ms = time_ms([&] {
-        hipLaunchKernelGGL((lde3_final_kernel<9, 0>), gf, dim3(NT), 0, 0, lde, n * cosets, n, cols, cosets,
-                           (const uint64_t*)tabs, L);
+        hipLaunchKernelGGL((lde3_final_kernel<9, 0>), gf, dim3(NT), 0, 0, lde, n * cosets, n, (size_t)0, 31u, cols,
+                           cosets, (const uint64_t*)tabs, L);
     });
     printf("{\"kernel\": \"final\", \"variant\": \"F1 in LDS, tabulated F2 prefetched\", \"ms\": %.3f}\n", ms);
     for (int v = 0; v < 7; v++) {
@@ -185,20 +185,21 @@ int main() {
     for (uint32_t nc : {0u, 1u, 4u}) {
         ms = time_ms([&] {
             hipLaunchKernelGGL((lde3_mid_kernel<9, true, true>), gm, dim3(NT), 0, 0, (const uint64_t*)scratch, n,
-                               scratch, n, lde, n * cosets, n, cols, nc, (const uint64_t*)inv, (const uint64_t*)tabs,
-                               L);
+                               scratch, n, lde, n * cosets, n, (size_t)0, 31u, cols, nc, (const uint64_t*)inv,
+                               (const uint64_t*)tabs, L);
         });
         printf("{\"kernel\": \"mid\", \"variant\": \"inverse + mono + %u cosets\", \"ms\": %.3f}\n", nc, ms);
         ms = time_ms([&] {
             hipLaunchKernelGGL((lde3_mid_kernel<9, true, false>), gm, dim3(NT), 0, 0, (const uint64_t*)scratch, n,
-                               scratch, n, lde, n * cosets, n, cols, nc, (const uint64_t*)inv, (const uint64_t*)tabs,
-                               L);
+                               scratch, n, lde, n * cosets, n, (size_t)0, 31u, cols, nc, (const uint64_t*)inv,
+                               (const uint64_t*)tabs, L);
         });
         printf("{\"kernel\": \"mid\", \"variant\": \"inverse + %u cosets (no mono)\", \"ms\": %.3f}\n", nc, ms);
     }
     ms = time_ms([&] {
         hipLaunchKernelGGL((lde3_mid_kernel<9, false, false>), gm, dim3(NT), 0, 0, (const uint64_t*)scratch, n,
-                           scratch, n, lde, n * cosets, n, cols, cosets, (const uint64_t*)inv, (const uint64_t*)tabs, L);
+                           scratch, n, lde, n * cosets, n, (size_t)0, 31u, cols, cosets, (const uint64_t*)inv,
+                           (const uint64_t*)tabs, L);
     });
     printf("{\"kernel\": \"mid\", \"variant\": \"monomial source, 4 cosets\", \"ms\": %.3f}\n", ms);
     CHECK(hipFree(scratch));
