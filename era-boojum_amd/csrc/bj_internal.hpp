@@ -105,6 +105,13 @@ hipError_t launch_lde3(uint64_t* lde, size_t col_stride, size_t coset_stride, ui
                        size_t src_stride, uint64_t* mono, size_t mono_stride, uint32_t n_cols, uint32_t log_n,
                        const uint64_t* inv_tab, const uint64_t* tabs, size_t tab_stride, hipStream_t st,
                        uint32_t log_k = 31, size_t block_stride = 0, uint32_t parts = LDE3_MID | LDE3_FINAL);
+// the inverse tail on the inverse head's output src, folded by F = 2^log_f (1..3) for `shards`
+// targets: dst + P * dst_shard_stride + c * dst_col_stride receives column c's monomials folded
+// with s_pow_m[P] (launch_fold_all's output), the monomials themselves never written
+bool lde3_inv_fold_supported(uint32_t log_n, uint32_t log_f, uint32_t shards);
+hipError_t launch_lde3_inv_fold(uint64_t* dst, size_t dst_col_stride, size_t dst_shard_stride, const uint64_t* src,
+                                size_t src_stride, uint32_t n_cols, uint32_t log_n, uint32_t log_f, uint32_t shards,
+                                const uint64_t* s_pow_m, const uint64_t* inv_tab, hipStream_t st);
 }  // namespace bj
 
 namespace bj {
@@ -132,4 +139,12 @@ bool lde_fused_supported(uint32_t log_n);
 int lde_fused_blocks(const uint64_t* trace, uint32_t n_cols, size_t trace_stride, uint32_t log_n, uint32_t log_lde,
                      uint32_t log_k, uint64_t* scratch, uint64_t* lde, size_t col_stride, size_t block_stride,
                      hipStream_t st);
+// capi.hip: the sender-side fold of the trace's monomials for `targets` shards without writing the
+// monomials (the inverse head into scratch, n_cols * 2^log_n words, then launch_lde3_inv_fold): target
+// T of column c at dst + T * dst_shard_stride + c * dst_col_stride, folded with s_pow_m[T] --
+// launch_fold_all's output.  inverse_fold_supported false: use bj_lde_coeffs_d + launch_fold_all.
+bool inverse_fold_supported(uint32_t log_n, uint32_t log_f, uint32_t targets);
+int inverse_fold_all(const uint64_t* trace, uint32_t n_cols, size_t trace_stride, uint32_t log_n, uint32_t log_f,
+                     uint32_t targets, const uint64_t* s_pow_m, uint64_t* scratch, size_t scratch_stride,
+                     uint64_t* dst, size_t dst_col_stride, size_t dst_shard_stride, hipStream_t st);
 }  // namespace bj

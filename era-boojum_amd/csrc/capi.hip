@@ -396,6 +396,24 @@ int lde_fused_blocks(const uint64_t* trace, uint32_t n_cols, size_t trace_stride
     return BJ_OK;
 }
 
+bool inverse_fold_supported(uint32_t log_n, uint32_t log_f, uint32_t targets) {
+    return use_lde3(log_n) && lde3_inv_fold_supported(log_n, log_f, targets);
+}
+
+int inverse_fold_all(const uint64_t* trace, uint32_t n_cols, size_t trace_stride, uint32_t log_n, uint32_t log_f,
+                     uint32_t targets, const uint64_t* s_pow_m, uint64_t* scratch, size_t scratch_stride,
+                     uint64_t* dst, size_t dst_col_stride, size_t dst_shard_stride, hipStream_t st) {
+    if (!inverse_fold_supported(log_n, log_f, targets)) return fail(BJ_EINVAL, "internal: unsupported inverse fold");
+    if (n_cols == 0) return BJ_OK;
+    const uint64_t* inv;
+    if (int r = get_ct(log_n, true, 1, &inv)) return r;
+    HIP_TRY(launch_ct_inverse_head(scratch, scratch_stride, trace, trace_stride, n_cols, log_n, inv, st), "ifft");
+    HIP_TRY(launch_lde3_inv_fold(dst, dst_col_stride, dst_shard_stride, scratch, scratch_stride, n_cols, log_n, log_f,
+                            targets, s_pow_m, inv, st),
+            "ifft fold");
+    return BJ_OK;
+}
+
 uint64_t shard_shift(uint32_t log_n, uint32_t log_lde, uint32_t log_shards, uint32_t shard) {
     return ::shard_shift(log_n, log_lde, log_shards, shard);
 }

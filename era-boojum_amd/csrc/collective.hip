@@ -648,7 +648,7 @@ int bj_sharded_commit_d(bj_comm* comm, const uint64_t* trace_shard, size_t trace
         HIP_CHECK(in.make(K), "hipEventCreate");
         HIP_CHECK(arrived.make(K), "hipEventCreate");
     }
-    std::vector<uint64_t> spm(world);
+    std::vector<uint64_t> spm((size_t)B * world);
     // phases 0 inverse (+ fold), 1 lde, 2 leaves, 3 nodes (bj_comm_set_timing)
     if (!comm->intervals.empty()) fold_intervals(comm, false);
     PhaseTimer pt(comm, st);
@@ -664,13 +664,19 @@ int bj_sharded_commit_d(bj_comm* comm, const uint64_t* trace_shard, size_t trace
             uint64_t* snd = send + (size_t)world * B * m * r.lo;
             uint64_t* mine = own + (size_t)r.lo * n;
             BJ_CHECK(pt.begin(0));
-            BJ_CHECK(bj_lde_coeffs_d(tr, r.count, trace_stride, log_n, mine, n, st));
-            for (uint32_t j = 0; j < B; j++) {
-                for (uint32_t p = 0; p < world; p++)
-                    spm[p] = gl::pow(bj::shard_shift(log_n, log_lde, ls, j * world + p), m);
-                HIP_CHECK(bj::launch_fold_all(snd + (size_t)j * world * r.count * m, m, (size_t)r.count * m, mine, n,
-                                              r.count, log2u(m), log_f, world, spm.data(), st),
-                          "fold");
+            // targets T = j G + p (block j, rank p) sit at snd + T r.count m: one stride
+            for (uint32_t T = 0; T < B * world; T++) spm[T] = gl::pow(bj::shard_shift(log_n, log_lde, ls, T), m);
+            if (bj::inverse_fold_supported(log_n, log_f, B * world)) {
+                // the inverse tail folds for every target straight from registers (ntt_lde3.hip)
+                BJ_CHECK(bj::inverse_fold_all(tr, r.count, trace_stride, log_n, log_f, B * world, spm.data(), mine, n,
+                                              snd, m, (size_t)r.count * m, st));
+            } else {
+                BJ_CHECK(bj_lde_coeffs_d(tr, r.count, trace_stride, log_n, mine, n, st));
+                for (uint32_t j = 0; j < B; j++)
+                    HIP_CHECK(bj::launch_fold_all(snd + (size_t)j * world * r.count * m, m, (size_t)r.count * m, mine,
+                                                  n, r.count, log2u(m), log_f, world, spm.data() + (size_t)j * world,
+                                                  st),
+                              "fold");
             }
             BJ_CHECK(pt.end());
             if (world > 1) {

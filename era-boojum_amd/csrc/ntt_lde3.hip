@@ -334,6 +334,91 @@ __global__ __launch_bounds__(NT, 2) void lde3_mid_kernel(const uint64_t* src, si
     }
 }
 
+// ------------------------------------------------------------- inverse tail + fold
+//
+// The collective commit's sender-side fold (collective.hip, G > D shards; shard.hip's
+// fold_all_kernel on ct_tail_kernel<true, true>'s monomials) straight from the inverse tail's
+// registers: for each target P < shards, h_u = sum_b c[u F + b] z[P F + b], u < n / F, canonical,
+// at dst + P dst_shard_stride.  The F terms of an output are registers F i .. F i + F - 1 of one
+// thread (block position l = 32 t + k), so the monomials never reach memory (C3 at G = 8: the
+// inverse + fold 2.30 -> 1.95 ms per rank, profiles/r4u_probe_ab.log).  Each target's 8192 / F
+// outputs of the block go out coalesced through one of two LDS halves (slot w + w / 32: the
+// writes w = (32 / F) t + i and the reads w = t + 256 k are both conflict-free), one barrier per
+// target.
+constexpr uint32_t kInvFoldConsts = 256;
+struct InvFoldZ {
+    uint64_t z[kInvFoldConsts];  // z[P F + bitrev_F(a)] = (s_P^m)^a
+};
+
+template <int R, int LOG_F>
+__global__ __launch_bounds__(NT, 2) void lde3_inv_fold_kernel(const uint64_t* src, size_t src_stride, uint64_t* dst,
+                                                              size_t dst_col_stride, size_t dst_shard_stride,
+                                                              uint32_t n_cols, uint32_t shards,
+                                                              const uint64_t* __restrict__ inv_tab, InvFoldZ zc) {
+    __shared__ uint64_t lds[PAD_LDS];
+    const uint32_t t = threadIdx.x;
+    const uint32_t c = __builtin_amdgcn_readfirstlane(blockIdx.x % n_cols);
+    const uint32_t q = __builtin_amdgcn_readfirstlane(blockIdx.x / n_cols);
+    uint64_t x[PT];
+    {
+        const auto rb = uniform_rsrc(src + (size_t)c * src_stride + (size_t)q * TILE, 8u * TILE);
+#pragma unroll
+        for (int k = 0; k < PT; k++)
+            x[k] = from_u32x2(__builtin_amdgcn_raw_buffer_load_b64(rb, (int)(t * 8), k * 2048, 0));
+    }
+    inverse_tail13<R>(x, inv_tab, q, t, lds);
+    // x[k] = c_j at block position l = 32 t + k; output u = (8192 q + 32 t) / F + i of every target
+    {
+        constexpr uint32_t F = 1u << LOG_F, OUTS = PT / F, BLK = TILE / F, HALF = PAD_LDS / 2;
+        static_assert(OUTS % 4 == 0 && BLK + BLK / 32 <= HALF, "fold layout");
+        __syncthreads();  // the tail's last LDS reads are done before the halves are written
+#pragma unroll 1
+        for (uint32_t P = 0; P < shards; P++) {
+            uint64_t h[OUTS];
+#pragma unroll
+            for (uint32_t i = 0; i < OUTS; i++) h[i] = x[F * i];
+#pragma unroll
+            for (uint32_t b = 1; b < F; b++) {
+                const uint64_t zb = zc.z[P * F + b];
+                const uint32_t z0 = (uint32_t)zb, z1 = (uint32_t)(zb >> 32);
+#pragma unroll
+                for (uint32_t i = 0; i < OUTS; i += 4) {
+                    uint32_t p0[4], p1[4], s0[4], s1[4];
+                    glasm::mul_sb_x4((uint32_t)x[F * i + b], (uint32_t)(x[F * i + b] >> 32), z0, z1, p0[0], p1[0],
+                                     (uint32_t)x[F * (i + 1) + b], (uint32_t)(x[F * (i + 1) + b] >> 32), z0, z1, p0[1],
+                                     p1[1], (uint32_t)x[F * (i + 2) + b], (uint32_t)(x[F * (i + 2) + b] >> 32), z0, z1,
+                                     p0[2], p1[2], (uint32_t)x[F * (i + 3) + b], (uint32_t)(x[F * (i + 3) + b] >> 32),
+                                     z0, z1, p0[3], p1[3]);
+                    glasm::add_x4((uint32_t)h[i], (uint32_t)(h[i] >> 32), p0[0], p1[0], s0[0], s1[0],
+                                  (uint32_t)h[i + 1], (uint32_t)(h[i + 1] >> 32), p0[1], p1[1], s0[1], s1[1],
+                                  (uint32_t)h[i + 2], (uint32_t)(h[i + 2] >> 32), p0[2], p1[2], s0[2], s1[2],
+                                  (uint32_t)h[i + 3], (uint32_t)(h[i + 3] >> 32), p0[3], p1[3], s0[3], s1[3]);
+#pragma unroll
+                    for (int j = 0; j < 4; j++) h[i + j] = join2(s0[j], s1[j]);
+                }
+            }
+#pragma unroll
+            for (uint32_t i = 0; i < OUTS; i += 4) canon4(h + i);
+            uint64_t* buf = lds + (P & 1) * HALF;
+#pragma unroll
+            for (uint32_t i = 0; i < OUTS; i++) {
+                const uint32_t w = OUTS * t + i;
+                buf[w + (w >> 5)] = h[i];
+            }
+            __syncthreads();
+            const auto rs = uniform_rsrc(dst + (size_t)P * dst_shard_stride + (size_t)c * dst_col_stride +
+                                             (size_t)q * BLK,
+                                         8u * BLK);
+#pragma unroll
+            for (uint32_t k = 0; k < OUTS; k++) {
+                const uint32_t w = t + NT * k;
+                __builtin_amdgcn_raw_buffer_store_b64(as_u32x2(buf[w + (w >> 5)]), rs, (int)(t * 8), (int)(k * 2048),
+                                                      0);
+            }
+        }
+    }
+}
+
 // ------------------------------------------------------------------- final pass
 //
 // Region T of a coset's column: element (q, o) at q' W + o (q' the middle pass's row rotation),
@@ -607,6 +692,58 @@ hipError_t launch_lde3(uint64_t* lde, size_t col_stride, size_t coset_stride, ui
         default: BJ_LDE3(10); break;
     }
 #undef BJ_LDE3
+    return hipGetLastError();
+}
+
+namespace {
+template <int R>
+void launch_lde3_inv_fold_R(uint64_t* dst, size_t dst_col_stride, size_t dst_shard_stride, const uint64_t* src,
+                            size_t src_stride, uint32_t n_cols, uint32_t log_f, uint32_t shards,
+                            const uint64_t* inv_tab, const InvFoldZ& zc, hipStream_t st) {
+    const dim3 g(n_cols << R);
+#define BJ_INV(LF)                                                                                             \
+    hipLaunchKernelGGL((lde3_inv_fold_kernel<R, LF>), g, dim3(NT), 0, st, src, src_stride, dst, dst_col_stride, \
+                       dst_shard_stride, n_cols, shards, inv_tab, zc)
+    switch (log_f) {
+        case 1: BJ_INV(1); break;
+        case 2: BJ_INV(2); break;
+        default: BJ_INV(3); break;
+    }
+#undef BJ_INV
+}
+}  // namespace
+
+bool lde3_inv_fold_supported(uint32_t log_n, uint32_t log_f, uint32_t shards) {
+    return lde3_supported(log_n) && log_f >= 1 && log_f <= 3 && shards >= 1 &&
+           (size_t)shards << log_f <= kInvFoldConsts;
+}
+
+hipError_t launch_lde3_inv_fold(uint64_t* dst, size_t dst_col_stride, size_t dst_shard_stride, const uint64_t* src,
+                                size_t src_stride, uint32_t n_cols, uint32_t log_n, uint32_t log_f, uint32_t shards,
+                                const uint64_t* s_pow_m, const uint64_t* inv_tab, hipStream_t st) {
+    if (n_cols == 0) return hipSuccess;
+    if (!lde3_inv_fold_supported(log_n, log_f, shards)) return hipErrorInvalidValue;
+    if (((uint64_t)n_cols << (log_n - 13)) > 0xffffffffull / NT) return hipErrorInvalidValue;
+    InvFoldZ zc{};
+    const uint32_t F = 1u << log_f;
+    for (uint32_t P = 0; P < shards; P++) {
+        uint64_t acc = 1;
+        for (uint32_t a = 0; a < F; a++) {
+            zc.z[P * F + gl::bitrev32(a, log_f)] = acc;
+            acc = gl::mul(acc, s_pow_m[P]);
+        }
+    }
+#define BJ_INVR(RR) \
+    launch_lde3_inv_fold_R<RR>(dst, dst_col_stride, dst_shard_stride, src, src_stride, n_cols, log_f, shards, inv_tab, zc, st)
+    switch (log_n - 13) {
+        case 5: BJ_INVR(5); break;
+        case 6: BJ_INVR(6); break;
+        case 7: BJ_INVR(7); break;
+        case 8: BJ_INVR(8); break;
+        case 9: BJ_INVR(9); break;
+        default: BJ_INVR(10); break;
+    }
+#undef BJ_INVR
     return hipGetLastError();
 }
 

@@ -154,6 +154,11 @@ def run_local(torch, world, n_cols, log_n, log_lde, cap, hasher, log_k=None):
     # G = 2 D in the three-pass range: half a coset per rank, the sender's fold
     (8, (16, 18, 2, 16, "poseidon2")),
     (8, (8, 19, 2, 4, "blake2s")),
+    # the inverse tail folding from registers (ntt_lde3.hip lde3_inv_kernel) at F = 4 and 8, and
+    # over B = 2 blocks of cosets (targets j G + p)
+    (8, (16, 18, 1, 16, "poseidon2")),        # F = 4
+    (8, (16, 18, 1, 16, "poseidon2", 0)),     # F = 8, B = 2
+    (8, (16, 18, 3, 32, "poseidon2", 2)),     # F = 2, B = 2
 ])
 def test_native_sharded_commit_local_ranks(torch_mod, world, cfg):
     n_cols, log_n, log_lde, cap, hasher = cfg[:5]

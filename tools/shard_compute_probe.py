@@ -6,7 +6,7 @@ leaves and subtree alone.  The result bounds the multi-GPU step time from below 
 hidden).  It is not a bench line: the received buffers are never filled, so the values are not
 a commitment.
 
-usage: python tools/shard_compute_probe.py [config ...]      (default: C3 at G = 1, 2, 4, 8 and
+usage: python tools/shard_compute_probe.py [config[:G] ...] (default: C3 at G = 1, 2, 4, 8 and
                                                                C4 at G = 8, one coset per rank)
 """
 import json
@@ -102,7 +102,8 @@ def main():
     from boojum_amd.sharded import NativeComm, NativeShardedResult, native_columns, native_sharded_commit
     plan = [("C3", 1), ("C3", 2), ("C3", 4), ("C3", 8), ("C4", 8)]
     if len(sys.argv) > 1:
-        plan = [(c, w) for c, w in plan if c in sys.argv[1:]]
+        # "C3" selects every world of a config, "C3:8" one world
+        plan = [(c, w) for c, w in plan if c in sys.argv[1:] or "%s:%d" % (c, w) in sys.argv[1:]]
     out = {}
     for cfg, world in plan:
         n_cols, log_n, log_lde, cap = bench.CONFIGS[cfg]
