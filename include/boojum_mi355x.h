@@ -372,8 +372,9 @@ int bj_comm_phase_ms(bj_comm* comm, float* ms_out4, int* calls_out);
 #define BJ_HASHER_KECCAK256 2
 
 /* Which global trace columns rank `shard` of G = 2^log_shards holds, in the order of its
- * trace_shard rows: the column pipeline deals chunk k (G * c_k consecutive columns, c = u, u,
- * 2u, 4u, ... capped at 32 rounded to u, u = 8 / gcd(8, G)) as G runs of c_k; when n_cols / G
+ * trace_shard rows: the column pipeline deals chunk k (G * c_k consecutive columns, u = 8 /
+ * gcd(8, G), c = u, u, then 3/2 (G <= 4) or 2 (G >= 8) times the previous rounded down to u but
+ * at least u more, capped at 32 rounded to u) as G runs of c_k; when n_cols / G
  * is not a multiple of u, or the hasher cannot be continued over column ranges (Keccak256),
  * rank P holds columns [P * n_cols / G, (P + 1) * n_cols / G).  cols_out: n_cols / G entries.
  * Host only (no device call). */

@@ -6,7 +6,8 @@ schedule in Python over torch.distributed (gloo) with the oracle's CPU steps
 partition math the native call implements:
 
   * the column deal (chunk k = G c_k consecutive columns, rank P the P-th run of c_k,
-    c = u, u, 2u, 4u, ... capped at 32, u = 8 / gcd(8, G); one contiguous chunk otherwise) --
+    u = 8 / gcd(8, G), c = u, u, then x3/2 (G <= 4) or x2 (G >= 8) rounded down to u but at
+    least u more, capped at 32; one contiguous chunk otherwise) --
     compared with bj_sharded_columns by tests/test_native_columns.py;
   * the LDE at D = 2^log_lde committed over its first k = 2^log_k cosets (prover.rs:313-347):
     rank P owns leaf range [P m, (P+1) m), m = k n / G, and the same range of every block of k
@@ -37,7 +38,7 @@ def chunk_unit(world):
     return 8 // math.gcd(8, world)
 
 
-def chunk_schedule(cols_per_rank, unit, max_cols=MAX_CHUNK_COLS):
+def chunk_schedule(cols_per_rank, unit, max_cols=MAX_CHUNK_COLS, world=8):
     max_cols = max(unit, max_cols // unit * unit)
     sched, done, b = [], 0, unit
     while done < cols_per_rank:
@@ -45,7 +46,7 @@ def chunk_schedule(cols_per_rank, unit, max_cols=MAX_CHUNK_COLS):
         sched.append(take)
         done += take
         if len(sched) >= 2:
-            b = min(2 * b, max_cols)
+            b = min(max(b + unit, b * 3 // 2 // unit * unit) if world <= 4 else 2 * b, max_cols)
     return sched
 
 
@@ -93,7 +94,7 @@ class ShardModel:
             raise ValueError("each shard needs more leaves than its cap slice")
         unit = chunk_unit(world)
         self.pipelined = world > 1 and self.cols_per_rank % unit == 0 and hasher in PARTIAL_HASHERS
-        self.schedule = chunk_schedule(self.cols_per_rank, unit, max_chunk_cols) if self.pipelined \
+        self.schedule = chunk_schedule(self.cols_per_rank, unit, max_chunk_cols, world) if self.pipelined \
             else [self.cols_per_rank]
         self.n_chunks = len(self.schedule)
         self.fold_exchange = bool(fold_exchange) and log_g > log_lde
