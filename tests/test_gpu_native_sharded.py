@@ -159,6 +159,11 @@ def run_local(torch, world, n_cols, log_n, log_lde, cap, hasher, log_k=None):
     (8, (16, 18, 1, 16, "poseidon2")),        # F = 4
     (8, (16, 18, 1, 16, "poseidon2", 0)),     # F = 8, B = 2
     (8, (16, 18, 3, 32, "poseidon2", 2)),     # F = 2, B = 2
+    # G <= D in the three-pass range: the monomials all-gathered, whole cosets per rank
+    (2, (16, 18, 2, 16, "poseidon2")),
+    (4, (16, 18, 2, 16, "poseidon2")),        # one coset per rank
+    (4, (16, 19, 3, 32, "blake2s")),          # two cosets per rank
+    (2, (16, 18, 3, 32, "poseidon2", 1)),     # G = k < D, B = 4
 ])
 def test_native_sharded_commit_local_ranks(torch_mod, world, cfg):
     n_cols, log_n, log_lde, cap, hasher = cfg[:5]
