@@ -102,10 +102,11 @@ __device__ __forceinline__ u32x2 as_u32x2(uint64_t v) {
 }
 __device__ __forceinline__ uint64_t from_u32x2(u32x2 v) { return ((uint64_t)v.y << 32) | v.x; }
 
-// x[k] *= f[k] for k < 16
-__device__ __forceinline__ void prescale16(uint64_t* x, const uint64_t* f) {
+// x[k] *= f[k] for k < K (K a multiple of 4)
+template <int K>
+__device__ __forceinline__ void prescale_n(uint64_t* x, const uint64_t* f) {
 #pragma unroll
-    for (int k = 0; k < 16; k += 4) {
+    for (int k = 0; k < K; k += 4) {
         uint32_t z0[4], z1[4];
         glasm::mul_x4((uint32_t)x[k], (uint32_t)(x[k] >> 32), (uint32_t)f[k], (uint32_t)(f[k] >> 32), z0[0], z1[0],
                       (uint32_t)x[k + 1], (uint32_t)(x[k + 1] >> 32), (uint32_t)f[k + 1], (uint32_t)(f[k + 1] >> 32),
@@ -290,8 +291,10 @@ __global__ __launch_bounds__(NT, 2) void lde3_mid_kernel(const uint64_t* src, si
         __syncthreads();  // the previous coset's (or the monomial epilogue's) LDS reads are done
 #pragma unroll
         for (int k = 0; k < PT; k++) lds[b1 + cbrev(k, 5)] = y[k];
-        // phase B's first 16 factors ahead of the barrier, the other 16 after the first products
-        // (64 VGPRs of factors next to the monomials and the phase's values spill)
+        // phase B's factors in quarters of 8, two in flight (64 VGPRs of factors next to the
+        // monomials and the phase's values spill): quarters 0, 1 ahead of the barrier, quarter
+        // q + 2 issued once quarter q's products are formed, so each load has a quarter's
+        // products to land behind
         const uint64_t* hb = tab + L3_HB + 32 * g5;
 #pragma unroll
         for (int k = 0; k < 16; k++) f[k] = hb[k];
@@ -299,14 +302,19 @@ __global__ __launch_bounds__(NT, 2) void lde3_mid_kernel(const uint64_t* src, si
 #pragma unroll
         for (int k = 0; k < PT; k++) y[k] = lds[b2 + 33 * cbrev(k, 5)];
         // phase B (stages 5..9): group g5, coefficient distance n / 1024
-        prescale16(y, f);
+        prescale_n<8>(y, f);
 #pragma unroll
-        for (int k = 16; k < PT; k++) f[k] = hb[k];
-        prescale16(y + 16, f + 16);
+        for (int k = 16; k < 24; k++) f[k] = hb[k];
+        prescale_n<8>(y + 8, f + 8);
+#pragma unroll
+        for (int k = 24; k < PT; k++) f[k] = hb[k];
+        prescale_n<8>(y + 16, f + 16);
+        prescale_n<8>(y + 24, f + 24);
         dft_p2<5, false, 0>(y);
 #pragma unroll
         for (int k = 0; k < PT; k++) lds[b2 + 33 * cbrev(k, 5)] = y[k];
         // phase C's factors (28: the first of each group of 8 is 1), issued before the barrier
+        // (ahead of phase B's DFT they spill 26 VGPRs)
         load28_c(f, tab + L3_C + 32 * t);
         __syncthreads();
 #pragma unroll
