@@ -209,14 +209,27 @@ __global__ __launch_bounds__(NT, 2) void ct_head_kernel(uint64_t* dst, size_t ds
     const uint32_t pd = 33 * W * s + w + (w >> 5);
 #pragma unroll
     for (int k = 0; k < PT; k++) lds[pa + 264 * k] = x[k];
-    if constexpr (P2 && R > 5) load32(f, ct + n + EXT_HB + 32 * s);
+    // phase B' factors in quarters of 8, two in flight: quarters 0, 1 ahead of the barrier,
+    // quarter q + 2 once quarter q's products are formed (ntt_lde3.hip's phase B)
+    const uint64_t* hb = ct + n + EXT_HB + 32 * s;
+    if constexpr (P2 && R > 5) {
+#pragma unroll
+        for (int k = 0; k < 16; k++) f[k] = hb[k];
+    }
     __syncthreads();
 #pragma unroll
     for (int k = 0; k < PT; k++) x[k] = lds[pd + k * W + ((k * W) >> 5)];
     if constexpr (P2) {
         // rows 32 s + k: groups of 2^(R-5) rows after phase A', coefficient distance n >> R
         if constexpr (R > 5) {
-            prescale32(x, f);
+            prescale_n<8>(x, f);
+#pragma unroll
+            for (int k = 16; k < 24; k++) f[k] = hb[k];
+            prescale_n<8>(x + 8, f + 8);
+#pragma unroll
+            for (int k = 24; k < PT; k++) f[k] = hb[k];
+            prescale_n<8>(x + 16, f + 16);
+            prescale_n<8>(x + 24, f + 24);
             dft_p2_groups<R - 5, INV>(x);
         }
     } else {

@@ -129,6 +129,22 @@ __device__ __forceinline__ void load32(uint64_t* r, const uint64_t* __restrict__
     for (int k = 0; k < PT; k++) r[k] = f[k];
 }
 
+// x[k] *= f[k] for k < K (K a multiple of 4)
+template <int K>
+__device__ __forceinline__ void prescale_n(uint64_t* x, const uint64_t* f) {
+#pragma unroll
+    for (int k = 0; k < K; k += 4) {
+        uint32_t z0[4], z1[4];
+        glasm::mul_x4((uint32_t)x[k], (uint32_t)(x[k] >> 32), (uint32_t)f[k], (uint32_t)(f[k] >> 32), z0[0], z1[0],
+                      (uint32_t)x[k + 1], (uint32_t)(x[k + 1] >> 32), (uint32_t)f[k + 1], (uint32_t)(f[k + 1] >> 32),
+                      z0[1], z1[1], (uint32_t)x[k + 2], (uint32_t)(x[k + 2] >> 32), (uint32_t)f[k + 2],
+                      (uint32_t)(f[k + 2] >> 32), z0[2], z1[2], (uint32_t)x[k + 3], (uint32_t)(x[k + 3] >> 32),
+                      (uint32_t)f[k + 3], (uint32_t)(f[k + 3] >> 32), z0[3], z1[3]);
+#pragma unroll
+        for (int i = 0; i < 4; i++) x[k + i] = join2(z0[i], z1[i]);
+    }
+}
+
 // x[k] *= f[k] for k < 32 (general products; outputs any u64 representative)
 __device__ __forceinline__ void prescale32(uint64_t* x, const uint64_t* f) {
 #pragma unroll

@@ -102,22 +102,6 @@ __device__ __forceinline__ u32x2 as_u32x2(uint64_t v) {
 }
 __device__ __forceinline__ uint64_t from_u32x2(u32x2 v) { return ((uint64_t)v.y << 32) | v.x; }
 
-// x[k] *= f[k] for k < K (K a multiple of 4)
-template <int K>
-__device__ __forceinline__ void prescale_n(uint64_t* x, const uint64_t* f) {
-#pragma unroll
-    for (int k = 0; k < K; k += 4) {
-        uint32_t z0[4], z1[4];
-        glasm::mul_x4((uint32_t)x[k], (uint32_t)(x[k] >> 32), (uint32_t)f[k], (uint32_t)(f[k] >> 32), z0[0], z1[0],
-                      (uint32_t)x[k + 1], (uint32_t)(x[k + 1] >> 32), (uint32_t)f[k + 1], (uint32_t)(f[k + 1] >> 32),
-                      z0[1], z1[1], (uint32_t)x[k + 2], (uint32_t)(x[k + 2] >> 32), (uint32_t)f[k + 2],
-                      (uint32_t)(f[k + 2] >> 32), z0[2], z1[2], (uint32_t)x[k + 3], (uint32_t)(x[k + 3] >> 32),
-                      (uint32_t)f[k + 3], (uint32_t)(f[k + 3] >> 32), z0[3], z1[3]);
-#pragma unroll
-        for (int i = 0; i < 4; i++) x[k + i] = join2(z0[i], z1[i]);
-    }
-}
-
 // y[k] = x[bitrev_5(k)] * h[k] with h wave-uniform (the phase-A factors s^((n/32) k), one table per
 // coset): the factors stay in SGPRs (scalar loads, mul_sb_x4), so they take no VGPRs next to the
 // monomials, the phase's values and its output
@@ -136,23 +120,23 @@ __device__ __forceinline__ void prescale32_brev_uniform(uint64_t* y, const uint6
     }
 }
 
-// Phase C's factors of the middle pass, k = 8 g + j with j > 0 (j = 0 is 1): loaded to f[k]
-__device__ __forceinline__ void load28_c(uint64_t* f, const uint64_t* __restrict__ c) {
+// Phase C's factors of the middle pass, k = 8 g + j with j > 0 (j = 0 is 1): the e-th of the 28
+// (e = 7 g + j - 1) loaded to f[k], for E0 <= e < E1
+__device__ __forceinline__ constexpr int c_reg(int e) { return 8 * (e / 7) + e % 7 + 1; }
+template <int E0, int E1>
+__device__ __forceinline__ void load_c(uint64_t* f, const uint64_t* __restrict__ c) {
 #pragma unroll
-    for (int k = 0; k < PT; k++)
-        if (k & 7) f[k] = c[k];
+    for (int e = E0; e < E1; e++) f[c_reg(e)] = c[c_reg(e)];
 }
 
-// y[k] *= f[k] for the 28 registers k mod 8 != 0 (general products)
-__device__ __forceinline__ void prescale28_c(uint64_t* y, const uint64_t* f) {
+// y[k] *= f[k] for the registers of the 28 with E0 <= e < E1 (groups of 4; general products)
+template <int E0, int E1>
+__device__ __forceinline__ void prescale_c(uint64_t* y, const uint64_t* f) {
 #pragma unroll
-    for (int q = 0; q < 7; q++) {
+    for (int q = E0 / 4; q < E1 / 4; q++) {
         int k[4];
 #pragma unroll
-        for (int i = 0; i < 4; i++) {
-            const int e = 4 * q + i;         // e-th of the 28: group e / 7, j = e % 7 + 1
-            k[i] = 8 * (e / 7) + e % 7 + 1;
-        }
+        for (int i = 0; i < 4; i++) k[i] = c_reg(4 * q + i);
         uint32_t z0[4], z1[4];
         glasm::mul_x4((uint32_t)y[k[0]], (uint32_t)(y[k[0]] >> 32), (uint32_t)f[k[0]], (uint32_t)(f[k[0]] >> 32), z0[0],
                       z1[0], (uint32_t)y[k[1]], (uint32_t)(y[k[1]] >> 32), (uint32_t)f[k[1]],
@@ -189,11 +173,22 @@ __device__ __forceinline__ void inverse_tail13(uint64_t* x, const uint64_t* __re
     const uint32_t bb = tail_base_b(thi, tlo);
 #pragma unroll
     for (int k = 0; k < PT; k++) lds[ba + tail_off_a(k)] = x[k];
-    load32(f, ext + ext_tb(R) + ((((size_t)q << 5) | thi) << 5));
+    // the TB factors in quarters of 8 as the forward phase B's: two in flight, each landing
+    // behind a quarter's products
+    const uint64_t* tb = ext + ext_tb(R) + ((((size_t)q << 5) | thi) << 5);
+#pragma unroll
+    for (int k = 0; k < 16; k++) f[k] = tb[k];
     __syncthreads();
 #pragma unroll
     for (int k = 0; k < PT; k++) x[k] = lds[bb + tail_off_b(k)];
-    prescale32(x, f);
+    prescale_n<8>(x, f);
+#pragma unroll
+    for (int k = 16; k < 24; k++) f[k] = tb[k];
+    prescale_n<8>(x + 8, f + 8);
+#pragma unroll
+    for (int k = 24; k < PT; k++) f[k] = tb[k];
+    prescale_n<8>(x + 16, f + 16);
+    prescale_n<8>(x + 24, f + 24);
     dft_p2<5, true, 0>(x);
     tw_ct_tailC<10>(wa, inv_tab, R, q, t);
     // same slots as the reads just made by this thread: no barrier needed before the writes
@@ -313,9 +308,11 @@ __global__ __launch_bounds__(NT, 2) void lde3_mid_kernel(const uint64_t* src, si
         dft_p2<5, false, 0>(y);
 #pragma unroll
         for (int k = 0; k < PT; k++) lds[b2 + 33 * cbrev(k, 5)] = y[k];
-        // phase C's factors (28: the first of each group of 8 is 1), issued before the barrier
-        // (ahead of phase B's DFT they spill 26 VGPRs)
-        load28_c(f, tab + L3_C + 32 * t);
+        // phase C's factors (28: the first of each group of 8 is 1): the first 16 issued before
+        // the barrier (all 28 ahead of phase B's DFT spill 26 VGPRs), the other 12 once the
+        // first 8 products are formed
+        const uint64_t* fc = tab + L3_C + 32 * t;
+        load_c<0, 16>(f, fc);
         __syncthreads();
 #pragma unroll
         for (int k = 0; k < PT; k++) y[k] = lds[b3 + 264 * cbrev(k, 5)];
@@ -323,7 +320,10 @@ __global__ __launch_bounds__(NT, 2) void lde3_mid_kernel(const uint64_t* src, si
         // group G = 4 t + (k >> 3) times sigma_10(G)^((n / 8192) j), then an 8-point DFT with w_8
         // (the CT network's twiddles CT13[2^u + (m >> (13 - u))] are these factors' powers
         // times 8th roots of unity)
-        prescale28_c(y, f);
+        prescale_c<0, 8>(y, f);
+        load_c<16, 28>(f, fc);
+        prescale_c<8, 16>(y, f);
+        prescale_c<16, 28>(y, f);
         dft_p2_groups<3, false>(y);
         __syncthreads();
 #pragma unroll
