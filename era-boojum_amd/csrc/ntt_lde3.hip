@@ -106,17 +106,25 @@ __device__ __forceinline__ uint64_t from_u32x2(u32x2 v) { return ((uint64_t)v.y 
 // coset): the factors stay in SGPRs (scalar loads, mul_sb_x4), so they take no VGPRs next to the
 // monomials, the phase's values and its output
 __device__ __forceinline__ void prescale32_brev_uniform(uint64_t* y, const uint64_t* x, const uint64_t* __restrict__ h) {
+    // the factors 8 at a time (one 64-byte scalar load): a scalar load's wait cannot be deferred
+    // past the next one (lgkmcnt(0)), so fewer, wider loads halve the waits
 #pragma unroll
-    for (int k = 0; k < PT; k += 4) {
-        uint32_t z0[4], z1[4];
-        const uint64_t a0 = x[cbrev(k, 5)], a1 = x[cbrev(k + 1, 5)], a2 = x[cbrev(k + 2, 5)], a3 = x[cbrev(k + 3, 5)];
-        const uint64_t f0 = h[k], f1 = h[k + 1], f2 = h[k + 2], f3 = h[k + 3];
-        glasm::mul_sb_x4((uint32_t)a0, (uint32_t)(a0 >> 32), (uint32_t)f0, (uint32_t)(f0 >> 32), z0[0], z1[0],
-                         (uint32_t)a1, (uint32_t)(a1 >> 32), (uint32_t)f1, (uint32_t)(f1 >> 32), z0[1], z1[1],
-                         (uint32_t)a2, (uint32_t)(a2 >> 32), (uint32_t)f2, (uint32_t)(f2 >> 32), z0[2], z1[2],
-                         (uint32_t)a3, (uint32_t)(a3 >> 32), (uint32_t)f3, (uint32_t)(f3 >> 32), z0[3], z1[3]);
+    for (int k8 = 0; k8 < PT; k8 += 8) {
+        uint64_t hf[8];
 #pragma unroll
-        for (int i = 0; i < 4; i++) y[k + i] = join2(z0[i], z1[i]);
+        for (int i = 0; i < 8; i++) hf[i] = h[k8 + i];
+#pragma unroll
+        for (int k = k8; k < k8 + 8; k += 4) {
+            uint32_t z0[4], z1[4];
+            const uint64_t a0 = x[cbrev(k, 5)], a1 = x[cbrev(k + 1, 5)], a2 = x[cbrev(k + 2, 5)], a3 = x[cbrev(k + 3, 5)];
+            const uint64_t f0 = hf[k - k8], f1 = hf[k - k8 + 1], f2 = hf[k - k8 + 2], f3 = hf[k - k8 + 3];
+            glasm::mul_sb_x4((uint32_t)a0, (uint32_t)(a0 >> 32), (uint32_t)f0, (uint32_t)(f0 >> 32), z0[0], z1[0],
+                             (uint32_t)a1, (uint32_t)(a1 >> 32), (uint32_t)f1, (uint32_t)(f1 >> 32), z0[1], z1[1],
+                             (uint32_t)a2, (uint32_t)(a2 >> 32), (uint32_t)f2, (uint32_t)(f2 >> 32), z0[2], z1[2],
+                             (uint32_t)a3, (uint32_t)(a3 >> 32), (uint32_t)f3, (uint32_t)(f3 >> 32), z0[3], z1[3]);
+#pragma unroll
+            for (int i = 0; i < 4; i++) y[k + i] = join2(z0[i], z1[i]);
+        }
     }
 }
 
