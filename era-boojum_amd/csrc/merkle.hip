@@ -109,8 +109,10 @@ __device__ __forceinline__ void leaf_hash_body(const uint64_t* __restrict__ src,
     else store_canon4_at(s, 2, out + 4 * L);
 }
 
+// Three waves per SIMD (<= 168 VGPRs) is what keeps the permutation at its issue rate: the
+// compiler's own allocation of the peeled absorptions would otherwise take 173 and drop to two.
 template <bool HAS_IN, bool FINAL>
-__global__ __launch_bounds__(LEAF_THREADS) void leaf_hash_kernel(const uint64_t* __restrict__ src,
+__global__ __launch_bounds__(LEAF_THREADS) __attribute__((amdgpu_waves_per_eu(3, 3))) void leaf_hash_kernel(const uint64_t* __restrict__ src,
                                                                  size_t col_stride, uint32_t n_cols,
                                                                  size_t n_leaves, const uint64_t* cap_in,
                                                                  uint64_t* out) {

@@ -12,9 +12,10 @@
 // gfx950 formulation (same field values; every result is compared canonically):
 // * state element = (lo, hi) 32-bit halves of a u64 representative, one permutation per lane;
 // * linear layers run on "limbs": L = sum c_j lo_j and H = sum c_j hi_j in 64-bit lanes,
-//   so a linear combination never carries (coefficients here stay < 2^16); the round
-//   constant is added into the limbs, and one 4-instruction reduction
-//   (glasm::reduce_xN) turns (L, H) back into a u64 per element;
+//   so a linear combination never carries (coefficients here stay < 2^16), and one
+//   4-instruction reduction (glasm::reduce_xN) turns (L, H) back into a u64 per element;
+// * a full round's constant is one 64-bit add into L (the reduction takes any L < 2^64 - 2^40
+//   plus H < 2^40); a partial round's constant costs nothing or one add per limb (Sched);
 // * S-box multiplies are the interleaved inline-asm products of gl_asm.hpp.
 #pragma once
 #include "gl.hpp"
@@ -23,7 +24,7 @@
 namespace p2 {
 
 // Round constants split into 64-bit (value, 0) pairs so a scalar load yields an SGPR pair
-// that v_lshl_add_u64 adds to a limb directly.
+// that v_lshl_add_u64 adds to a limb directly (the quad-lane node form, poseidon2_quad.hpp).
 struct RcLimbs {
     uint64_t lo[30][12];
     uint64_t hi[30][12];
@@ -44,6 +45,95 @@ constexpr RcLimbs make_rc_limbs() {
 }
 
 __device__ __constant__ static const RcLimbs RCL = make_rc_limbs();
+
+// ---- The constant schedule (field values; every entry canonical, computed at compile time) ----
+//
+// The reference adds RC_r before round r's S-boxes (state_generic_impl.rs:131-138, 55-64).
+// * Full rounds: the limbs after an external MDS are L, H < 2^39; L + RC_r stays below
+//   2^64 - 2^40 for every full-round constant (checked below), where the reduction is still
+//   exact (reduce_stream: W = Hhi EPS + L < 2^64), so RC_r is one 64-bit add into L instead of
+//   a 32-bit limb add into each of L and H.
+// * Partial rounds run in pairs (partial_round_pair).  The first M_I of a pair adds a constant
+//   K to every element (its first limb-sum chain starts at K instead of 0, so K is free) and
+//   the second adds D to element 0 only (one add per limb).  The state then differs from the
+//   reference's by an offset vector f known at compile time; K and D are chosen so that f_0 is
+//   exactly the next partial round's constant whenever element 0 enters its S-box, and the
+//   first full round after the partial rounds adds RC_26 - f (rc26) instead of RC_26.
+//   RC_4 (the first partial constant) is added to element 0 before the reduction that ends the
+//   first full rounds.
+// tests/test_poseidon2_sched.py restates this derivation and checks it against the reference's
+// known answers.
+namespace sched {
+constexpr uint64_t P = 0xFFFFFFFF00000001ull;
+constexpr uint64_t addm(uint64_t a, uint64_t b) { return (uint64_t)(((unsigned __int128)a + b) % P); }
+constexpr uint64_t subm(uint64_t a, uint64_t b) { return addm(a, P - b % P); }
+constexpr uint64_t mulm(uint64_t a, uint64_t b) { return (uint64_t)(((unsigned __int128)a * b) % P); }
+constexpr int SH[12] = {4, 14, 11, 8, 0, 5, 2, 9, 13, 6, 3, 12};
+// A 64-bit constant added into L: L < 2^39 after an external MDS, so L + c < 2^64 - 2^40
+// whenever c < 2^64 - 2^41.
+constexpr uint64_t FULL_RC_BOUND = ~0ull - (1ull << 41) + 1;
+// After the last partial round L, H < 2^61 (mi_layer_b_limbs), so W = Hhi EPS + L + c < 2^64
+// whenever c < 2^64 - 2^62; larger entries of rc26 go in as 32-bit limbs.
+constexpr uint64_t LIMB_RC_BOUND = (1ull << 63) + (1ull << 62);
+struct Values {
+    uint64_t k[11];     // per partial pair: first M_I's constant (every element)
+    uint64_t d[10];     // per partial pair but the last: second M_I's constant (element 0)
+    uint64_t rc26[12];  // RC_26 - f
+};
+constexpr Values derive() {
+    Values v{};
+    // the offset f of the state against the reference's, entering each pair: f_0 = rc_r
+    uint64_t f[12] = {RC_FLAT[4][0]};
+    for (int q = 0; q < 11; q++) {
+        const int r = 4 + 2 * q;
+        uint64_t s = 0;  // element 0 leaves its S-box exact: offset only on 1..11
+        for (int i = 1; i < 12; i++) s = addm(s, f[i]);
+        v.k[q] = subm(RC_FLAT[r + 1][0], s);
+        f[0] = 0;
+        for (int i = 0; i < 12; i++) f[i] = addm(addm(mulm(f[i], 1ull << SH[i]), s), v.k[q]);
+        s = 0;
+        for (int i = 1; i < 12; i++) s = addm(s, f[i]);
+        f[0] = 0;
+        for (int i = 0; i < 12; i++) f[i] = addm(mulm(f[i], 1ull << SH[i]), s);
+        if (q < 10) {
+            v.d[q] = subm(RC_FLAT[r + 2][0], f[0]);
+            f[0] = RC_FLAT[r + 2][0];
+        }
+    }
+    for (int i = 0; i < 12; i++) v.rc26[i] = subm(RC_FLAT[26][i], f[i]);
+    return v;
+}
+constexpr Values V = derive();
+constexpr bool full_rcs_fit() {
+    for (int r : {0, 1, 2, 3, 27, 28, 29})
+        for (int i = 0; i < 12; i++)
+            if (RC_FLAT[r][i] >= FULL_RC_BOUND) return false;
+    return RC_FLAT[4][0] < FULL_RC_BOUND;
+}
+static_assert(full_rcs_fit(), "a full-round constant is too large for the one-add form");
+}  // namespace sched
+
+// The schedule's device tables: full words, and (value, 0) limb pairs for the asm layers.
+struct Sched {
+    uint64_t rcw[30][12];                   // RC_FLAT as 64-bit words (full rounds, RC_4[0])
+    uint64_t k_lo[11], k_hi[11];
+    uint64_t d_lo[10], d_hi[10];
+    uint64_t rc26_w[12], rc26_lo[12], rc26_hi[12];
+};
+constexpr Sched make_sched() {
+    Sched s{};
+    for (int r = 0; r < 30; r++)
+        for (int i = 0; i < 12; i++) s.rcw[r][i] = RC_FLAT[r][i];
+    for (int q = 0; q < 11; q++) { s.k_lo[q] = sched::V.k[q] & 0xFFFFFFFFull; s.k_hi[q] = sched::V.k[q] >> 32; }
+    for (int q = 0; q < 10; q++) { s.d_lo[q] = sched::V.d[q] & 0xFFFFFFFFull; s.d_hi[q] = sched::V.d[q] >> 32; }
+    for (int i = 0; i < 12; i++) {
+        s.rc26_w[i] = sched::V.rc26[i];
+        s.rc26_lo[i] = sched::V.rc26[i] & 0xFFFFFFFFull;
+        s.rc26_hi[i] = sched::V.rc26[i] >> 32;
+    }
+    return s;
+}
+__device__ __constant__ static const Sched SCH = make_sched();
 
 struct State {
     uint32_t lo[12], hi[12];
@@ -83,6 +173,14 @@ __device__ __forceinline__ void m4_limbs(uint64_t& x0, uint64_t& x1, uint64_t& x
     uint64_t t6 = t3 + t5;
     uint64_t t7 = t2 + t4;
     x0 = t6; x1 = t5; x2 = t7; x3 = t4;
+}
+
+// lo + b as a 64-bit limb in one v_mad_u64_u32 (lo * 1 + b): no zero-extended register pair
+// for lo.  b is wave-uniform (a round-constant limb in an SGPR pair).
+__device__ __forceinline__ uint64_t add_lo_u64(uint32_t lo, uint64_t b) {
+    uint64_t r;
+    asm volatile("v_mad_u64_u32 %0, vcc, %1, 1, %2" : "=v"(r) : "v"(lo), "s"(b) : "vcc");
+    return r;
 }
 
 // Which outputs of a permutation its caller reads: all 12 (bj_poseidon2_permute), the capacity
@@ -139,14 +237,13 @@ __device__ __forceinline__ void reduce12(const uint64_t* L, const uint64_t* H, u
 }
 
 // Full round r on the pending limbs (L, H) of the state (the external MDS of the previous
-// step not yet reduced): reduce(L + RC_r, H + RC_r), x^7, then the external MDS into
-// new pending limbs.  Leaves the reduced S-box output in s.
-template <int OUT = OUT_ALL>
+// step not yet reduced): reduce(L + RC_r, H) (Sched: one 64-bit add per element), x^7, then
+// the external MDS into new pending limbs.  Leaves the reduced S-box output in s.
+template <int OUT = OUT_ALL, bool RC = true>
 __device__ __forceinline__ void full_round(State& s, uint64_t* L, uint64_t* H, int r) {
+    if constexpr (RC) {
 #pragma unroll
-    for (int i = 0; i < 12; i++) {
-        L[i] += RCL.lo[r][i];
-        H[i] += RCL.hi[r][i];
+        for (int i = 0; i < 12; i++) L[i] += SCH.rcw[r][i];
     }
     reduce12(L, H, s.lo, s.hi);
 #pragma unroll
@@ -155,44 +252,60 @@ __device__ __forceinline__ void full_round(State& s, uint64_t* L, uint64_t* H, i
     mds_ext_limbs<OUT>(s.hi, H);
 }
 
-// lo + b as a 64-bit limb in one v_mad_u64_u32 (lo * 1 + b): no zero-extended register pair
-// for lo.  b is wave-uniform (a round-constant limb in an SGPR pair).
-__device__ __forceinline__ uint64_t add_lo_u64(uint32_t lo, uint64_t b) {
-    uint64_t r;
-    asm volatile("v_mad_u64_u32 %0, vcc, %1, 1, %2" : "=v"(r) : "v"(lo), "s"(b) : "vcc");
-    return r;
-}
-
-// Partial-round S-box on a reduced z: z += RC_r, z^7 as 32-bit halves (lo, hi).
-__device__ __forceinline__ void partial_sbox(uint64_t z, int r, uint32_t& lo, uint32_t& hi) {
-    const uint64_t L0 = add_lo_u64((uint32_t)z, RCL.lo[r][0]);
-    const uint64_t H0 = add_lo_u64((uint32_t)(z >> 32), RCL.hi[r][0]);
-    uint64_t y;
-    glasm::reduce_x1(L0, (uint32_t)H0, (uint32_t)(H0 >> 32), y);
-    split(y, lo, hi);
-    sbox_x1(lo, hi);
-}
-
-// Two partial rounds r, r + 1 on the state as 64-bit register pairs Z (the reductions' own
-// output pairs, so the loop carries no 32-bit copies).  M_I of round r leaves elements 1..11
-// as unreduced limbs (< 2^46.6); only s0, the next S-box input, is reduced.  Round r + 1's M_I
-// consumes the limbs (sums < 2^50.2, shifted terms < 2^61) and reduces every element.  Same
-// field values as two reduced rounds (glasm::mi_layer_a / mi_layer_b, tools/gen_gl_asm.py).
-__device__ __forceinline__ void partial_round_pair(uint64_t* Z, int r) {
+// Two partial rounds (pair q: rounds 4 + 2q, 5 + 2q) on the state as 64-bit register pairs Z
+// (the reductions' own output pairs, so the loop carries no 32-bit copies); Z[0] already holds
+// its round constant.  M_I of the first round leaves elements 1..11 as unreduced limbs
+// (< 2^46.6); only s0, the next S-box input, is reduced.  The second M_I consumes the limbs
+// (sums < 2^50.2, shifted terms < 2^61) and reduces every element.  Same field values as two
+// reduced rounds plus the schedule's offsets (glasm::mi_layer_a / mi_layer_b,
+// tools/gen_gl_asm.py).  The constants are read before the asm blocks (which the compiler does
+// not move loads across), so their scalar loads land during the first S-box.
+__device__ __forceinline__ void partial_round_pair(uint64_t* Z, int q) {
     uint64_t L[12], H[12], z0;
     uint32_t lo[12], hi[12];
+    const uint64_t kl = SCH.k_lo[q], kh = SCH.k_hi[q], dl = SCH.d_lo[q], dh = SCH.d_hi[q];
 #pragma unroll
-    for (int i = 1; i < 12; i++) split(Z[i], lo[i], hi[i]);
-    partial_sbox(Z[0], r, lo[0], hi[0]);
-    glasm::mi_layer_a(lo, hi, L, H, z0);
+    for (int i = 0; i < 12; i++) split(Z[i], lo[i], hi[i]);
+    sbox_x1(lo[0], hi[0]);
+    glasm::mi_layer_a(lo, hi, kl, kh, L, H, z0);
     uint32_t lo0, hi0;
-    partial_sbox(z0, r + 1, lo0, hi0);
-    glasm::mi_layer_b(lo0, hi0, L, H, Z);
+    split(z0, lo0, hi0);
+    sbox_x1(lo0, hi0);
+    glasm::mi_layer_b(lo0, hi0, L, H, dl, dh, Z);
+}
+
+// The last pair (rounds 24, 25): the second M_I hands its limbs to the first full round.
+__device__ __forceinline__ void partial_round_pair_last(const uint64_t* Z, uint64_t* Lo, uint64_t* Ho) {
+    uint64_t L[12], H[12], z0;
+    uint32_t lo[12], hi[12];
+    const uint64_t kl = SCH.k_lo[10], kh = SCH.k_hi[10];
+#pragma unroll
+    for (int i = 0; i < 12; i++) split(Z[i], lo[i], hi[i]);
+    sbox_x1(lo[0], hi[0]);
+    glasm::mi_layer_a(lo, hi, kl, kh, L, H, z0);
+    uint32_t lo0, hi0;
+    split(z0, lo0, hi0);
+    sbox_x1(lo0, hi0);
+    glasm::mi_layer_b_limbs(lo0, hi0, L, H, Lo, Ho);
+}
+
+// RC_26 - f into the limbs the last partial round left: one 64-bit add where the value allows
+// it (sched::LIMB_RC_BOUND), else one 32-bit limb add into each of L and H.
+template <int I = 0>
+__device__ __forceinline__ void add_rc26(uint64_t* L, uint64_t* H) {
+    if constexpr (sched::V.rc26[I] < sched::LIMB_RC_BOUND) {
+        L[I] += SCH.rc26_w[I];
+    } else {
+        L[I] += SCH.rc26_lo[I];
+        H[I] += SCH.rc26_hi[I];
+    }
+    if constexpr (I + 1 < 12) add_rc26<I + 1>(L, H);
 }
 
 // The permutation (state_generic_impl.rs:221-236): MDS; 4 x (RC, S-box, MDS);
-// 22 partial rounds; 4 x (RC, S-box, MDS).  OUT: the outputs the caller reads (the others are
-// left unspecified); the last full round is peeled so that its MDS forms only those.
+// 22 partial rounds; 4 x (RC, S-box, MDS), with the round constants placed by Sched.
+// OUT: the outputs the caller reads (the others are left unspecified); the last full round is
+// peeled so that its MDS forms only those.
 template <int OUT = OUT_ALL>
 __device__ __forceinline__ void permute(State& s) {
     uint64_t L[12], H[12], Z[12];
@@ -200,6 +313,7 @@ __device__ __forceinline__ void permute(State& s) {
     mds_ext_limbs(s.hi, H);
 #pragma unroll 1
     for (int r = 0; r < 4; r++) full_round(s, L, H, r);
+    L[0] += SCH.rcw[4][0];
 #pragma unroll
     for (int q = 0; q < 3; q++) {
         const int i = 4 * q;
@@ -209,14 +323,12 @@ __device__ __forceinline__ void permute(State& s) {
                          L[i + 3], (uint32_t)H[i + 3], (uint32_t)(H[i + 3] >> 32), Z[i + 3]);
     }
 #pragma unroll 1
-    for (int r = 4; r < 26; r += 2) partial_round_pair(Z, r);
-#pragma unroll
-    for (int i = 0; i < 12; i++) {
-        L[i] = (uint32_t)Z[i];
-        H[i] = Z[i] >> 32;
-    }
+    for (int q = 0; q < 10; q++) partial_round_pair(Z, q);
+    partial_round_pair_last(Z, L, H);
+    add_rc26(L, H);
+    full_round<OUT_ALL, false>(s, L, H, 26);
 #pragma unroll 1
-    for (int r = 26; r < 29; r++) full_round(s, L, H, r);
+    for (int r = 27; r < 29; r++) full_round(s, L, H, r);
     full_round<OUT>(s, L, H, 29);
     reduce12<OUT>(L, H, s.lo, s.hi);
 }

@@ -304,30 +304,44 @@ def _consts(pro):
     return consts, sreg
 
 
+# limb-sum chains per limb in the M_I layers (ILP against instruction count: k chains cost k - 1
+# combining adds).  One chain each measured fastest with tools/leaf_bench.hip (C3 leaf shape,
+# 2^22 leaves, alternated on one box, profiles/r5d_leaf_variants.log): 3 + 2 chains 33.70 ms,
+# 2 + 1 33.62, 1 + 1 33.57; three waves per SIMD cover the chains' latency.
+LAYER_A_CHAINS = 1
+LAYER_B_CHAINS = 1
+
+
 def emit_mi_layer_a():
     """First partial round of a pair: M_I with elements 1..11 left as unreduced limbs.
-    L_i = lo_i 2^SH[i] + sum lo_j, H_i likewise (one mad each, < 2^46.6); only element 0,
-    the next S-box input, is reduced (into the 64-bit z0).  The pair's second round
-    (mi_layer_b) reduces all."""
+    L_i = lo_i 2^SH[i] + sum lo_j + K_lo, H_i likewise (one mad each, < 2^46.6); only element
+    0, the next S-box input, is reduced (into the 64-bit z0).  The pair's second round
+    (mi_layer_b*) reduces all.  K (K_lo, K_hi: wave-uniform 64-bit SGPR pairs holding 32-bit
+    values) starts the first sum chain in place of 0, so it costs nothing: it adds the field
+    constant K_lo + K_hi 2^32 to every output.  poseidon2.hpp chooses K so that element 0 gets
+    the next partial round's constant and carries the offset the other elements pick up
+    (p2::Sched)."""
     pro = []
     consts, sreg = _consts(pro)
-    SUM = {("L", c): "v[%d:%d]" % (2 * c, 2 * c + 1) for c in range(3)}
-    SUM.update({("H", c): "v[%d:%d]" % (6 + 2 * c, 7 + 2 * c) for c in range(3)})
+    NC = LAYER_A_CHAINS
+    SUM = {("L", c): "v[%d:%d]" % (2 * c, 2 * c + 1) for c in range(NC)}
+    SUM.update({("H", c): "v[%d:%d]" % (6 + 2 * c, 7 + 2 * c) for c in range(NC)})
+    members = [[i for i in range(12) if i % NC == c] for c in range(NC)]
     chains = []
     for limb, src in (("L", "lo"), ("H", "hi")):
-        for c in range(3):
+        for c in range(NC):
             ch = []
-            for t in range(4):
-                i = 4 * c + t
+            for t, i in enumerate(members[c]):
                 acc = SUM[(limb, c)]
-                ch.append(("v_mad_u64_u32 %s, %s, %%[%s%d], 1, %s" % (acc, JUNK, src, i, "0" if t == 0 else acc),
+                start = ("%%[K%s]" % limb) if c == 0 else "0"
+                ch.append(("v_mad_u64_u32 %s, %s, %%[%s%d], 1, %s" % (acc, JUNK, src, i, start if t == 0 else acc),
                            set(), {JUNK}))
             chains.append(ch)
     body = pro + merge(chains)
     for limb in ("L", "H"):
         a = SUM[(limb, 0)]
-        body.append(("v_lshl_add_u64 %s, %s, 0, %s" % (a, SUM[(limb, 1)], a), set(), set()))
-        body.append(("v_lshl_add_u64 %s, %s, 0, %s" % (a, SUM[(limb, 2)], a), set(), set()))
+        for c in range(1, NC):
+            body.append(("v_lshl_add_u64 %s, %s, 0, %s" % (a, SUM[(limb, c)], a), set(), set()))
     Ls, Hs = SUM[("L", 0)], SUM[("H", 0)]
     for i in range(1, 12):
         K = consts.get(SH[i], str(1 << SH[i]))
@@ -337,33 +351,33 @@ def emit_mi_layer_a():
     body.append(("v_mad_u64_u32 v[14:15], %s, %%[hi0], %d, %s" % (JUNK, 1 << SH[0], Hs), set(), {JUNK}))
     body += reduce_limbs("v[12:13]", "v[14:15]", "v[16:17]", "v18", sp(0), "%[z0]")
     text = pad(body)
-    args = "const uint32_t* lo, const uint32_t* hi, uint64_t* L, uint64_t* H, uint64_t& z0"
+    args = "const uint32_t* lo, const uint32_t* hi, uint64_t KL, uint64_t KH, uint64_t* L, uint64_t* H, uint64_t& z0"
     outs = ['[z0] "=&v"(z0)']
     outs += ['[L%d] "=&v"(L[%d]), [H%d] "=&v"(H[%d])' % (i, i, i, i) for i in range(1, 12)]
     ins = ['[lo%d] "v"(lo[%d]), [hi%d] "v"(hi[%d])' % (i, i, i, i) for i in range(12)]
+    ins += ['[KL] "s"(KL)', '[KH] "s"(KH)']
     clob = ['"v%d"' % i for i in range(20)] + ['"s%d"' % i for i in range(SGPR_BASE, sreg)]
     n_v = sum(1 for t in text if t.startswith("v_"))
-    lines = ["// Poseidon2 partial round M_I, first of a pair: elements 1..11 as limbs L, H (%d VALU instructions)" % n_v,
+    lines = ["// Poseidon2 partial round M_I + K, first of a pair: elements 1..11 as limbs L, H (%d VALU instructions)" % n_v,
              "__device__ __forceinline__ void mi_layer_a(%s) {" % args, "    asm volatile("]
     lines += ['        "%s\\n"' % t for t in text]
     lines += ["        : %s" % ", ".join(outs), "        : %s" % ", ".join(ins), "        : %s);" % ", ".join(clob), "}"]
     return "\n".join(lines) + "\n"
 
 
-def emit_mi_layer_b():
-    """Second partial round of a pair: M_I on element 0 (reduced lo0, hi0) and elements 1..11
-    as the limbs L_i, H_i < 2^46.6 left by mi_layer_a.  Sums over limbs < 2^50.2;
-    L_i' = L_i << SH[i] + sum < 2^61 (one v_lshl_add_u64 when SH[i] <= MAX_LSHL_ADD_SHIFT,
-    else shift + add); then the 4-instruction reduction of every element into the 64-bit z[i]."""
-    pro = []
-    consts, sreg = _consts(pro)
+def _layer_b_sums(body):
+    """The limb sums of mi_layer_b*: element 0 (lo0, hi0) and the limbs L_i, H_i, i = 1..11,
+    into v[0:1] / v[2:3]; two chains per limb for ILP: (0, 1..5) and (6..11)."""
     Ls, Hs = "v[0:1]", "v[2:3]"
     Ls2, Hs2 = "v[4:5]", "v[6:7]"
-    body = list(pro)
-    # two chains per limb for ILP: (0, 1..5) and (6..11)
     chains = []
     for acc, acc2, src, lim in ((Ls, Ls2, "lo", "L"), (Hs, Hs2, "hi", "H")):
         ch = [("v_mad_u64_u32 %s, %s, %%[%s0], 1, %%[%s1]" % (acc, JUNK, src, lim), set(), {JUNK})]
+        if LAYER_B_CHAINS == 1:
+            for j in range(2, 12):
+                ch.append(("v_lshl_add_u64 %s, %%[%s%d], 0, %s" % (acc, lim, j, acc), set(), set()))
+            chains.append(ch)
+            continue
         for j in range(2, 6):
             ch.append(("v_lshl_add_u64 %s, %%[%s%d], 0, %s" % (acc, lim, j, acc), set(), set()))
         ch2 = [("v_lshl_add_u64 %s, %%[%s6], 0, %%[%s7]" % (acc2, lim, lim), set(), set())]
@@ -371,8 +385,43 @@ def emit_mi_layer_b():
             ch2.append(("v_lshl_add_u64 %s, %%[%s%d], 0, %s" % (acc2, lim, j, acc2), set(), set()))
         chains += [ch, ch2]
     body += merge(chains)
-    body.append(("v_lshl_add_u64 %s, %s, 0, %s" % (Ls, Ls2, Ls), set(), set()))
-    body.append(("v_lshl_add_u64 %s, %s, 0, %s" % (Hs, Hs2, Hs), set(), set()))
+    if LAYER_B_CHAINS == 2:
+        body.append(("v_lshl_add_u64 %s, %s, 0, %s" % (Ls, Ls2, Ls), set(), set()))
+        body.append(("v_lshl_add_u64 %s, %s, 0, %s" % (Hs, Hs2, Hs), set(), set()))
+    return Ls, Hs
+
+
+def _layer_b_term(i, Lp, Hp, Ls, Hs, corr=False):
+    """L_i' = L_i << SH[i] + sum (element 0: lo0 2^SH[0] + sum), H_i' likewise; with corr,
+    element 0 also gets the SGPR constant pair D (DL, DH)."""
+    st = []
+    if i == 0:
+        st.append(("v_mad_u64_u32 %s, %s, %%[lo0], %d, %s" % (Lp, JUNK, 1 << SH[0], Ls), set(), {JUNK}))
+        st.append(("v_mad_u64_u32 %s, %s, %%[hi0], %d, %s" % (Hp, JUNK, 1 << SH[0], Hs), set(), {JUNK}))
+        if corr:
+            st.append(("v_lshl_add_u64 %s, %s, 0, %%[DL]" % (Lp, Lp), set(), set()))
+            st.append(("v_lshl_add_u64 %s, %s, 0, %%[DH]" % (Hp, Hp), set(), set()))
+    else:
+        for P, lim, S in ((Lp, "L", Ls), (Hp, "H", Hs)):
+            if SH[i] <= MAX_LSHL_ADD_SHIFT:
+                st.append(("v_lshl_add_u64 %s, %%[%s%d], %d, %s" % (P, lim, i, SH[i], S), set(), set()))
+            else:
+                st.append(("v_lshlrev_b64 %s, %d, %%[%s%d]" % (P, SH[i], lim, i), set(), set()))
+                st.append(("v_lshl_add_u64 %s, %s, 0, %s" % (P, P, S), set(), set()))
+    return st
+
+
+def emit_mi_layer_b():
+    """Second partial round of a pair: M_I on element 0 (reduced lo0, hi0) and elements 1..11
+    as the limbs L_i, H_i < 2^46.6 left by mi_layer_a.  Sums over limbs < 2^50.2;
+    L_i' = L_i << SH[i] + sum < 2^61 (one v_lshl_add_u64 when SH[i] <= MAX_LSHL_ADD_SHIFT,
+    else shift + add); element 0 also gets the constant D (the next pair's first round
+    constant, less the offset the others carry: p2::Sched); then the 4-instruction reduction of
+    every element into the 64-bit z[i]."""
+    pro = []
+    consts, sreg = _consts(pro)
+    body = list(pro)
+    Ls, Hs = _layer_b_sums(body)
     for g in range(3):
         streams = []
         for j in range(4):
@@ -382,30 +431,49 @@ def emit_mi_layer_b():
             Hp = "v[%d:%d]" % (base + 2, base + 3)
             Wp = "v[%d:%d]" % (base + 4, base + 5)
             M = "v%d" % (base + 6)
-            c = sp(j)
-            st = []
-            if i == 0:
-                st.append(("v_mad_u64_u32 %s, %s, %%[lo0], %d, %s" % (Lp, JUNK, 1 << SH[0], Ls), set(), {JUNK}))
-                st.append(("v_mad_u64_u32 %s, %s, %%[hi0], %d, %s" % (Hp, JUNK, 1 << SH[0], Hs), set(), {JUNK}))
-            else:
-                for P, lim, S in ((Lp, "L", Ls), (Hp, "H", Hs)):
-                    if SH[i] <= MAX_LSHL_ADD_SHIFT:
-                        st.append(("v_lshl_add_u64 %s, %%[%s%d], %d, %s" % (P, lim, i, SH[i], S), set(), set()))
-                    else:
-                        st.append(("v_lshlrev_b64 %s, %d, %%[%s%d]" % (P, SH[i], lim, i), set(), set()))
-                        st.append(("v_lshl_add_u64 %s, %s, 0, %s" % (P, P, S), set(), set()))
-            st += reduce_limbs(Lp, Hp, Wp, M, c, "%%[z%d]" % i)
+            st = _layer_b_term(i, Lp, Hp, Ls, Hs, corr=True)
+            st += reduce_limbs(Lp, Hp, Wp, M, sp(j), "%%[z%d]" % i)
             streams.append(st)
         body += merge(streams)
     text = pad(body)
-    args = "uint32_t lo0, uint32_t hi0, const uint64_t* L, const uint64_t* H, uint64_t* z"
+    args = "uint32_t lo0, uint32_t hi0, const uint64_t* L, const uint64_t* H, uint64_t DL, uint64_t DH, uint64_t* z"
     outs = ['[z%d] "=&v"(z[%d])' % (i, i) for i in range(12)]
     ins = ['[lo0] "v"(lo0)', '[hi0] "v"(hi0)']
     ins += ['[L%d] "v"(L[%d]), [H%d] "v"(H[%d])' % (i, i, i, i) for i in range(1, 12)]
+    ins += ['[DL] "s"(DL)', '[DH] "s"(DH)']
     clob = ['"v%d"' % i for i in range(8 + 32)] + ['"s%d"' % i for i in range(SGPR_BASE, sreg)]
     n_v = sum(1 for t in text if t.startswith("v_"))
-    lines = ["// Poseidon2 partial round M_I, second of a pair: reduces every element (%d VALU instructions)" % n_v,
+    lines = ["// Poseidon2 partial round M_I + D e_0, second of a pair: reduces every element (%d VALU instructions)" % n_v,
              "__device__ __forceinline__ void mi_layer_b(%s) {" % args, "    asm volatile("]
+    lines += ['        "%s\\n"' % t for t in text]
+    lines += ["        : %s" % ", ".join(outs), "        : %s" % ", ".join(ins), "        : %s);" % ", ".join(clob), "}"]
+    return "\n".join(lines) + "\n"
+
+
+def emit_mi_layer_b_limbs():
+    """The last partial round (the second of the last pair): M_I as in mi_layer_b, but the
+    outputs stay limbs (L_i' < 2^61, H_i' likewise): the first full round after the partial
+    rounds adds its constants to them and reduces, so the pair's own 12 reductions (and the
+    moves that re-split reduced words into limbs) are not needed."""
+    pro = []
+    consts, sreg = _consts(pro)
+    body = list(pro)
+    Ls, Hs = _layer_b_sums(body)
+    for g in range(3):
+        streams = []
+        for j in range(4):
+            i = 4 * g + j
+            streams.append(_layer_b_term(i, "%%[Lo%d]" % i, "%%[Ho%d]" % i, Ls, Hs))
+        body += merge(streams)
+    text = pad(body)
+    args = "uint32_t lo0, uint32_t hi0, const uint64_t* L, const uint64_t* H, uint64_t* Lo, uint64_t* Ho"
+    outs = ['[Lo%d] "=&v"(Lo[%d]), [Ho%d] "=&v"(Ho[%d])' % (i, i, i, i) for i in range(12)]
+    ins = ['[lo0] "v"(lo0)', '[hi0] "v"(hi0)']
+    ins += ['[L%d] "v"(L[%d]), [H%d] "v"(H[%d])' % (i, i, i, i) for i in range(1, 12)]
+    clob = ['"v%d"' % i for i in range(8)] + ['"s%d"' % i for i in range(SGPR_BASE, sreg)]
+    n_v = sum(1 for t in text if t.startswith("v_"))
+    lines = ["// Poseidon2 last partial round M_I, outputs as limbs (%d VALU instructions)" % n_v,
+             "__device__ __forceinline__ void mi_layer_b_limbs(%s) {" % args, "    asm volatile("]
     lines += ['        "%s\\n"' % t for t in text]
     lines += ["        : %s" % ", ".join(outs), "        : %s" % ", ".join(ins), "        : %s);" % ", ".join(clob), "}"]
     return "\n".join(lines) + "\n"
@@ -459,6 +527,14 @@ def sgpr_operandize(fn_text):
 
 
 def main():
+    import argparse
+    global LAYER_A_CHAINS, LAYER_B_CHAINS
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--out", default=OUT, help="output header (variants for A/B builds elsewhere)")
+    ap.add_argument("--a-chains", type=int, default=LAYER_A_CHAINS, choices=(1, 2, 3, 4))
+    ap.add_argument("--b-chains", type=int, default=LAYER_B_CHAINS, choices=(1, 2))
+    args = ap.parse_args()
+    LAYER_A_CHAINS, LAYER_B_CHAINS = args.a_chains, args.b_chains
     parts = ['''// GENERATED by tools/gen_gl_asm.py -- do not edit.
 // gfx950 inline-asm Goldilocks primitives (see the generator's docstring for the
 // design and the hazard rule).  p = 2^64 - 2^32 + 1.  All values are (lo, hi) 32-bit
@@ -493,11 +569,12 @@ namespace glasm {
                              doc="%d canonicalisations z = x mod p in [0, p)" % n))
     parts.append(emit_mi_layer_a())
     parts.append(emit_mi_layer_b())
+    parts.append(emit_mi_layer_b_limbs())
     parts.append("}  // namespace glasm\n")
     parts = [sgpr_operandize(x) for x in parts]
-    with open(OUT, "w") as f:
+    with open(args.out, "w") as f:
         f.write("\n".join(parts))
-    print("wrote", OUT)
+    print("wrote", args.out)
 
 
 if __name__ == "__main__":
