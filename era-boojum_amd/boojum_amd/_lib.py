@@ -77,6 +77,8 @@ SIGNATURES = {
     "bj_comm_exchange_d": ([_vp, _int, _vp, _vp, _sz, _vp], _int),
     "bj_comm_set_timing": ([_vp, _int], _int),
     "bj_comm_phase_ms": ([_vp, ctypes.POINTER(ctypes.c_float), ctypes.POINTER(_int)], _int),
+    "bj_comm_info": ([_vp, _vp], _int),
+    "bj_comm_check_world": ([_vp, _vp, _vp], _int),
     "bj_sharded_columns": ([_u32, _u32, _u32, _int, ctypes.POINTER(_u32)], _int),
     "bj_sharded_commit_d": ([_vp, _vp, _sz, _u32, _u32, _u32, _u32, _u32, _int, _vp, _vp, _vp, _vp, _vp], _int),
     "bj_sharded_query_h": ([_vp, _vp, _vp, _vp, _u32, _u32, _u32, _u32, _u32, _int, _u64, _u64p, _u64p, _u64p,
@@ -85,6 +87,26 @@ SIGNATURES = {
     "bj_fill_synthetic_d": ([_vp, _u32, _sz, _u32, _u64, _u64, _vp], _int),
     "bj_gl_op_d": ([_int, _vp, _vp, _vp, _sz, _vp], _int),
 }
+
+
+
+class CommInfo(ctypes.Structure):
+    """bj_comm_info_t (include/boojum_mi355x.h), 128 bytes."""
+    _fields_ = [("kind", ctypes.c_int32), ("world", ctypes.c_int32), ("rank", ctypes.c_int32),
+                ("transport_count", ctypes.c_int32), ("transport_rank", ctypes.c_int32),
+                ("device", ctypes.c_int32), ("pci_bus_id", ctypes.c_char * 32), ("host", ctypes.c_char * 64),
+                ("reserved", ctypes.c_int32 * 2)]
+
+    KINDS = {0: "rccl", 1: "local", 2: "callback"}
+
+    def as_dict(self):
+        return {"kind": self.KINDS.get(self.kind, self.kind), "world": self.world, "rank": self.rank,
+                "transport_count": self.transport_count, "transport_rank": self.transport_rank,
+                "device": self.device, "pci_bus_id": self.pci_bus_id.decode(errors="replace"),
+                "host": self.host.decode(errors="replace")}
+
+
+assert ctypes.sizeof(CommInfo) == 128
 
 _LIB = None
 

@@ -79,6 +79,29 @@ class NativeComm:
     def __init__(self, handle, world, rank, keep=None):
         self.handle, self.world, self.rank, self._keep = handle, world, rank, keep
 
+    def info(self):
+        """bj_comm_info: what the transport reports for this rank (RCCL: ncclCommCount,
+        ncclCommUserRank, ncclCommCuDevice), with the device's PCI bus id and the host name."""
+        from ._lib import CommInfo
+        out = CommInfo()
+        check(load().bj_comm_info(self.handle, ctypes.byref(out)), "bj_comm_info")
+        return out.as_dict()
+
+    def check_world(self, stream=None):
+        """bj_comm_check_world (collective): every rank's info, gathered; raises BoojumError when
+        the transport's world is not this communicator's (count, rank order) or, for RCCL, when two
+        ranks drive one device.  Returns (ok, [info per rank], message)."""
+        from ._lib import BoojumError, CommInfo
+        out = (CommInfo * self.world)()
+        rc = load().bj_comm_check_world(self.handle, out, stream)
+        infos = [r.as_dict() for r in out]
+        if rc == 0:
+            return True, infos, ""
+        msg = load().bj_last_error().decode(errors="replace")
+        if rc != -22:
+            raise BoojumError("bj_comm_check_world: rc %d: %s" % (rc, msg))
+        return False, infos, msg
+
     @classmethod
     def _make(cls, fn, *args, world, rank, keep=None):
         h = ctypes.c_void_p()

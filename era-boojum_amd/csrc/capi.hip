@@ -467,7 +467,7 @@ hipError_t pool_alloc(void** p, size_t bytes, hipStream_t st) {
 extern "C" {
 
 const char* bj_last_error(void) { return g_err.c_str(); }
-uint32_t bj_abi_version(void) { return (2u << 16) | 4u; }
+uint32_t bj_abi_version(void) { return (2u << 16) | 5u; }
 
 int bj_release_workspace(void) {
     HIP_TRY(bj::pool_trim_all(), "hipMemPoolTrimTo");

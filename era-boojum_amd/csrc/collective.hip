@@ -19,6 +19,7 @@
 #include <hip/hip_runtime.h>
 #include <rccl/rccl.h>
 #include <dlfcn.h>
+#include <unistd.h>
 
 #include <algorithm>
 #include <condition_variable>
@@ -57,6 +58,11 @@ struct Rccl {
     decltype(&ncclGroupStart) group_start = nullptr;
     decltype(&ncclGroupEnd) group_end = nullptr;
     decltype(&ncclGetErrorString) error_string = nullptr;
+    // what the communicator itself reports (bj_comm_info); optional: a librccl without them
+    // still runs commits, and bj_comm_info then fails for RCCL communicators
+    decltype(&ncclCommCount) comm_count = nullptr;
+    decltype(&ncclCommUserRank) comm_user_rank = nullptr;
+    decltype(&ncclCommCuDevice) comm_cu_device = nullptr;
     bool ok = false;
     std::string why;
 };
@@ -90,6 +96,9 @@ const Rccl& rccl() {
         RCCL_SYM(group_end, "ncclGroupEnd")
         RCCL_SYM(error_string, "ncclGetErrorString")
 #undef RCCL_SYM
+        r.comm_count = reinterpret_cast<decltype(r.comm_count)>(dlsym(h, "ncclCommCount"));
+        r.comm_user_rank = reinterpret_cast<decltype(r.comm_user_rank)>(dlsym(h, "ncclCommUserRank"));
+        r.comm_cu_device = reinterpret_cast<decltype(r.comm_cu_device)>(dlsym(h, "ncclCommCuDevice"));
         r.ok = true;
     });
     return r;
@@ -142,6 +151,7 @@ struct LocalGroup {
 struct bj_comm {
     enum Kind { RCCL_OWNED, RCCL_WRAPPED, LOCAL, CALLBACK } kind;
     int world = 1, rank = 0;
+    int device = -1;  // the device current when the communicator was made (bj_comm_info)
     ncclComm_t nccl = nullptr;
     LocalGroup* group = nullptr;
     bj_exchange_fn fn = nullptr;  // CALLBACK: the caller's exchange
@@ -456,6 +466,7 @@ int bj_comm_init_rccl(const uint8_t* id128, int world, int rank, bj_comm** out) 
     ncclComm_t comm = nullptr;
     RCCL_CHECK(R, R.init_rank(&comm, world, id, rank), "ncclCommInitRank");
     bj_comm* c = new bj_comm();
+    (void)hipGetDevice(&c->device);
     c->kind = bj_comm::RCCL_OWNED;
     c->world = world;
     c->rank = rank;
@@ -471,6 +482,7 @@ int bj_comm_wrap_rccl(void* nccl_comm, int world, int rank, bj_comm** out) {
     const Rccl& R = rccl();
     if (!R.ok) return err(BJ_EHIP, R.why);
     bj_comm* c = new bj_comm();
+    (void)hipGetDevice(&c->device);
     c->kind = bj_comm::RCCL_WRAPPED;
     c->world = world;
     c->rank = rank;
@@ -514,6 +526,7 @@ int bj_comm_init_local(void* group, int rank, bj_comm** out) {
     if (!g || !out) return err(BJ_EINVAL, "null argument");
     if (rank < 0 || rank >= g->world) return err(BJ_EINVAL, "rank out of range");
     bj_comm* c = new bj_comm();
+    (void)hipGetDevice(&c->device);
     c->kind = bj_comm::LOCAL;
     c->world = g->world;
     c->rank = rank;
@@ -527,6 +540,7 @@ int bj_comm_init_callback(int world, int rank, bj_exchange_fn fn, void* user, in
     if (world < 1 || !is_pow2((uint64_t)world) || rank < 0 || rank >= world)
         return err(BJ_EINVAL, "world must be a power of two and 0 <= rank < world");
     bj_comm* c = new bj_comm();
+    (void)hipGetDevice(&c->device);
     c->kind = bj_comm::CALLBACK;
     c->world = world;
     c->rank = rank;
@@ -567,6 +581,84 @@ int bj_comm_exchange_d(bj_comm* c, int kind, const void* send, void* recv, size_
     if (bytes && (!send || !recv)) return err(BJ_EINVAL, "null buffer");
     hipStream_t st = reinterpret_cast<hipStream_t>(stream);
     return kind == BJ_XCHG_ALL_GATHER ? all_gather(c, send, recv, bytes, st) : all_to_all(c, send, recv, bytes, st);
+}
+
+int bj_comm_info(bj_comm* c, bj_comm_info_t* out) {
+    if (!c || !out) return err(BJ_EINVAL, "null argument");
+    std::memset(out, 0, sizeof(*out));
+    out->world = c->world;
+    out->rank = c->rank;
+    out->transport_count = c->world;
+    out->transport_rank = c->rank;
+    out->device = c->device;
+    if (is_rccl(c)) {
+        out->kind = BJ_COMM_RCCL;
+        const Rccl& R = rccl();
+        if (!R.comm_count || !R.comm_user_rank || !R.comm_cu_device)
+            return err(BJ_EHIP, "librccl.so.1 does not export ncclCommCount / ncclCommUserRank / ncclCommCuDevice");
+        RCCL_CHECK(R, R.comm_count(c->nccl, &out->transport_count), "ncclCommCount");
+        RCCL_CHECK(R, R.comm_user_rank(c->nccl, &out->transport_rank), "ncclCommUserRank");
+        RCCL_CHECK(R, R.comm_cu_device(c->nccl, &out->device), "ncclCommCuDevice");
+    } else {
+        out->kind = c->kind == bj_comm::LOCAL ? BJ_COMM_LOCAL : BJ_COMM_CALLBACK;
+    }
+    // the bus id names the physical device; a device number this process cannot open (a stand-in
+    // transport's) leaves it empty
+    if (hipDeviceGetPCIBusId(out->pci_bus_id, (int)sizeof(out->pci_bus_id) - 1, out->device) != hipSuccess) {
+        out->pci_bus_id[0] = 0;
+        (void)hipGetLastError();
+    }
+    if (gethostname(out->host, sizeof(out->host) - 1) != 0) out->host[0] = 0;
+    return BJ_OK;
+}
+
+int bj_comm_check_world(bj_comm* c, bj_comm_info_t* all_out, void* stream) {
+    if (!c || !all_out) return err(BJ_EINVAL, "null argument");
+    static_assert(sizeof(bj_comm_info_t) == 128, "bj_comm_info_t is 128 bytes");
+    bj_comm_info_t mine;
+    BJ_CHECK(bj_comm_info(c, &mine));
+    hipStream_t st = reinterpret_cast<hipStream_t>(stream);
+    const size_t rec = sizeof(bj_comm_info_t);
+    void* dev = nullptr;
+    HIP_CHECK(hipMalloc(&dev, rec * (c->world + 1)), "hipMalloc");
+    char* send = static_cast<char*>(dev) + rec * c->world;
+    int rc = BJ_OK;
+    hipError_t e = hipMemcpyAsync(send, &mine, rec, hipMemcpyHostToDevice, st);
+    if (e == hipSuccess) {
+        rc = all_gather(c, send, dev, rec, st);
+        if (rc == BJ_OK) e = hipMemcpyAsync(all_out, dev, rec * c->world, hipMemcpyDeviceToHost, st);
+        if (rc == BJ_OK && e == hipSuccess) e = hipStreamSynchronize(st);
+    }
+    (void)hipFree(dev);
+    if (rc) return rc;
+    if (e != hipSuccess) return err(BJ_EHIP, std::string("bj_comm_check_world: ") + hipGetErrorString(e));
+    // what the transport saw: every rank in its own slot, the transport's count and rank equal to
+    // the communicator's; an RCCL world with one device per rank (the local and callback
+    // transports may share a device by design: ranks as threads, a rehearsal over gloo)
+    for (int p = 0; p < c->world; p++) {
+        const bj_comm_info_t& r = all_out[p];
+        if (r.world != c->world || r.rank != p || r.transport_count != c->world || r.transport_rank != p)
+            return err(BJ_EINVAL, "bj_comm_check_world: slot " + std::to_string(p) + " holds rank " +
+                                      std::to_string(r.rank) + " of " + std::to_string(r.world) + ", transport rank " +
+                                      std::to_string(r.transport_rank) + " of " + std::to_string(r.transport_count) +
+                                      " (expected rank " + std::to_string(p) + " of " + std::to_string(c->world) + ")");
+    }
+    if (mine.kind == BJ_COMM_RCCL) {
+        for (int p = 0; p < c->world; p++)
+            for (int q = 0; q < p; q++) {
+                const bj_comm_info_t &a = all_out[q], &b = all_out[p];
+                const bool same_host = std::strncmp(a.host, b.host, sizeof(a.host)) == 0;
+                const bool same_dev = a.pci_bus_id[0] && b.pci_bus_id[0]
+                                          ? std::strncmp(a.pci_bus_id, b.pci_bus_id, sizeof(a.pci_bus_id)) == 0
+                                          : a.device == b.device;
+                if (same_host && same_dev)
+                    return err(BJ_EINVAL, "bj_comm_check_world: ranks " + std::to_string(q) + " and " +
+                                              std::to_string(p) + " share device " + std::to_string(a.device) +
+                                              (a.pci_bus_id[0] ? std::string(" (") + a.pci_bus_id + ")" : std::string()) +
+                                              " on " + a.host);
+            }
+    }
+    return BJ_OK;
 }
 
 int bj_comm_destroy(bj_comm* c) {

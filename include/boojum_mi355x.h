@@ -350,6 +350,32 @@ int bj_comm_local_group_destroy(void* group);
 int bj_comm_init_local(void* group, int rank, bj_comm** out);
 int bj_comm_init_callback(int world, int rank, bj_exchange_fn exchange, void* user, int host_staged, bj_comm** out);
 int bj_comm_destroy(bj_comm* comm);
+/* What a communicator's transport sees (ABI 2.5; no reference counterpart: the reference has no
+ * collectives).  kind: BJ_COMM_RCCL / BJ_COMM_LOCAL / BJ_COMM_CALLBACK; world, rank: as the
+ * communicator was made; transport_count, transport_rank, device: RCCL's own ncclCommCount,
+ * ncclCommUserRank and ncclCommCuDevice (the other transports: world, rank and the device current
+ * when the communicator was made); pci_bus_id: hipDeviceGetPCIBusId of that device ("" when this
+ * process cannot open it); host: gethostname.  128 bytes. */
+#define BJ_COMM_RCCL 0
+#define BJ_COMM_LOCAL 1
+#define BJ_COMM_CALLBACK 2
+typedef struct bj_comm_info_t {
+    int32_t kind;
+    int32_t world, rank;
+    int32_t transport_count, transport_rank;
+    int32_t device;
+    char pci_bus_id[32];
+    char host[64];
+    int32_t reserved[2];
+} bj_comm_info_t;
+int bj_comm_info(bj_comm* comm, bj_comm_info_t* out);
+/* Collective over `comm` (ordered on `stream`, as bj_comm_exchange_d): all-gathers every rank's
+ * bj_comm_info_t into all_out[world] and checks the world the transport formed: slot p holds rank
+ * p, and every rank's transport count and rank equal the communicator's world and rank; for RCCL
+ * also that no two ranks drive one device (same host and PCI bus id, or same device number where
+ * the bus id is unknown).  BJ_EINVAL naming the ranks otherwise (all_out is filled either way once
+ * the gather ran).  The local and callback transports may share a device by design. */
+int bj_comm_check_world(bj_comm* comm, bj_comm_info_t* all_out, void* stream);
 /* One data exchange of bj_sharded_commit_d's kinds (BJ_XCHG_ALL_GATHER / BJ_XCHG_ALL_TO_ALL, the
  * layouts above) over `comm`, ordered on `stream`: the transport alone, so a caller can check its
  * communicator before a commit.  Collective; bytes per rank block, a multiple of 8.  An RCCL

@@ -226,6 +226,7 @@ typedef struct {
     const uint8_t* uid;     /* RCCL (bj_comm_init_rccl) over this unique id */
     int rank, world;
     uint32_t n_cols, log_n, log_lde, log_k, cap;
+    int check_world;        /* RCCL: 1 expect bj_comm_check_world to pass, -1 to reject a shared device */
     const u64* trace; /* all columns, host */
     u64* leaves;      /* all leaves, host: rank P writes its range */
     u64* cap_out;     /* this rank's gathered cap */
@@ -268,6 +269,34 @@ static void* rank_worker(void* p) {
     bj_comm* comm = NULL;
     j->rc = j->group ? bj_comm_init_local(j->group, j->rank, &comm) : bj_comm_init_rccl(j->uid, j->world, j->rank, &comm);
     if (j->rc) return NULL;
+    if (j->check_world) {
+        /* what RCCL's API reports for this rank (ncclCommCount / UserRank / CuDevice), then the
+         * collective world check: a shared device must be rejected, distinct ones accepted */
+        bj_comm_info_t info, all[64];
+        j->rc = bj_comm_info(comm, &info);
+        if (j->rc) return NULL;
+        if (info.kind != BJ_COMM_RCCL || info.transport_count != j->world || info.transport_rank != j->rank ||
+            info.world != j->world || info.rank != j->rank) {
+            fprintf(stderr, "rank %d: bj_comm_info kind %d world %d rank %d transport %d of %d\n", j->rank, info.kind,
+                    info.world, info.rank, info.transport_rank, info.transport_count);
+            j->rc = -1;
+            return NULL;
+        }
+        int rc = bj_comm_check_world(comm, all, st);
+        if (j->check_world > 0 ? rc != BJ_OK : rc != BJ_EINVAL || !strstr(bj_last_error(), "share device")) {
+            fprintf(stderr, "rank %d: bj_comm_check_world rc %d (%s), expected %s\n", j->rank, rc, bj_last_error(),
+                    j->check_world > 0 ? "success" : "a shared-device rejection");
+            j->rc = -1;
+            return NULL;
+        }
+        for (int p = 0; p < j->world; p++)
+            if (all[p].rank != p || all[p].transport_count != j->world) {
+                fprintf(stderr, "rank %d: gathered slot %d holds rank %d of %d\n", j->rank, p, all[p].rank,
+                        all[p].transport_count);
+                j->rc = -1;
+                return NULL;
+            }
+    }
     j->rc = bj_sharded_commit_d(comm, tr, n, j->n_cols, j->log_n, j->log_lde, j->log_k, j->cap, BJ_HASHER_POSEIDON2,
                                 lde, leaves, nodes, cap, st);
     if (j->rc == 0) {
@@ -286,7 +315,7 @@ static void* rank_worker(void* p) {
  * the mock librccl.so.1 (tests/c/mock_rccl.cpp, BJ_TEST_MOCK_RCCL), since RCCL refuses two ranks
  * on one device */
 static void check_sharded(uint32_t log_n, uint32_t n_cols, uint32_t log_lde, uint32_t log_k, uint32_t cap, int world,
-                          int use_rccl) {
+                          int use_rccl, int check_world) {
     size_t n = (size_t)1 << log_n, nd = n << log_lde, nl = n << log_k, n_nodes = nl - cap;
     u64* trace = xmalloc(8 * n * n_cols);
     for (uint32_t c = 0; c < n_cols; c++)
@@ -300,7 +329,7 @@ static void check_sharded(uint32_t log_n, uint32_t n_cols, uint32_t log_lde, uin
     pthread_t th[64];
     rank_job_t jobs[64];
     for (int P = 0; P < world; P++) {
-        jobs[P] = (rank_job_t){group, uid, P, world, n_cols, log_n, log_lde, log_k, cap, trace, leaves,
+        jobs[P] = (rank_job_t){group, uid, P, world, n_cols, log_n, log_lde, log_k, cap, check_world, trace, leaves,
                                caps + 4 * (size_t)cap * P, 0};
         pthread_create(&th[P], NULL, rank_worker, &jobs[P]);
     }
@@ -401,16 +430,29 @@ int main(int argc, char** argv) {
         fprintf(stderr, "cannot load %s: %s\n", mock, dlerror());
         return 2;
     }
+    int worlds_checked = 0;
     for (int world = 2; world <= 8; world *= 2)
         if (n_cols % world == 0 && ((size_t)1 << (log_n + log_k)) / world > (cap / world ? cap / world : 1)) {
-            check_sharded(log_n, n_cols, log_lde, log_k, cap, world, 0);
-            if (mock) check_sharded(log_n, n_cols, log_lde, log_k, cap, world, 1);
+            check_sharded(log_n, n_cols, log_lde, log_k, cap, world, 0, 0);
+            if (mock) {
+                /* the stand-in's ranks share this GPU: the world check must name the shared device;
+                 * with distinct (stand-in) device numbers it must pass */
+                check_sharded(log_n, n_cols, log_lde, log_k, cap, world, 1, -1);
+                setenv("MOCK_RCCL_FAKE_DEVICES", "1", 1);
+                check_sharded(log_n, n_cols, log_lde, log_k, cap, world, 1, 1);
+                unsetenv("MOCK_RCCL_FAKE_DEVICES");
+                worlds_checked |= world;
+            }
         }
     check_errors();
     if (failures) {
         fprintf(stderr, "%d check(s) failed\n", failures);
         return 1;
     }
+    if (mock)
+        printf("rccl world check ok at world%s%s%s: ncclCommCount = world, ncclCommUserRank = rank, shared device "
+               "rejected, distinct devices accepted\n", worlds_checked & 2 ? " 2" : "", worlds_checked & 4 ? " 4" : "",
+               worlds_checked & 8 ? " 8" : "");
     printf("c_caller ok%s: 2^%u x %u, LDE x%u, %u cosets committed, cap %u, %d seam threads; "
            "cap[0] = %016llx %016llx %016llx %016llx\n",
            mock ? " (collective also over RCCL's API, mock librccl)" : "", log_n, n_cols, 1u << log_lde, 1u << log_k, cap,

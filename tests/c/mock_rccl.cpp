@@ -22,6 +22,7 @@
 
 #include <condition_variable>
 #include <cstdio>
+#include <cstdlib>
 #include <cstring>
 #include <map>
 #include <mutex>
@@ -93,6 +94,7 @@ thread_local hipStream_t t_stream = nullptr;
 struct ncclComm {
     Group* g;
     int rank;
+    int device;  // ncclCommCuDevice: the calling thread's device, or the rank with MOCK_RCCL_FAKE_DEVICES=1
 };
 
 namespace {
@@ -220,7 +222,33 @@ ncclResult_t ncclCommInitRank(ncclComm_t* comm, int nranks, ncclUniqueId id, int
     }
     if (g->world != nranks) return ncclInvalidUsage;
     g->barrier();  // ncclCommInitRank is collective
-    *comm = new ncclComm{g, rank};
+    // The ranks of this stand-in are threads on one GPU, so ncclCommCuDevice reports that device
+    // for all of them (what bj_comm_check_world must reject as a duplicated device); with
+    // MOCK_RCCL_FAKE_DEVICES=1 at init it reports device = rank instead, a world of distinct
+    // devices as a real one-process-per-GPU run has.
+    int dev = 0;
+    (void)hipGetDevice(&dev);
+    const char* fake = getenv("MOCK_RCCL_FAKE_DEVICES");
+    if (fake && fake[0] == '1') dev = rank;
+    *comm = new ncclComm{g, rank, dev};
+    return ncclSuccess;
+}
+
+ncclResult_t ncclCommCount(const ncclComm_t comm, int* count) {
+    if (!comm || !count) return ncclInvalidArgument;
+    *count = comm->g->world;
+    return ncclSuccess;
+}
+
+ncclResult_t ncclCommUserRank(const ncclComm_t comm, int* rank) {
+    if (!comm || !rank) return ncclInvalidArgument;
+    *rank = comm->rank;
+    return ncclSuccess;
+}
+
+ncclResult_t ncclCommCuDevice(const ncclComm_t comm, int* device) {
+    if (!comm || !device) return ncclInvalidArgument;
+    *device = comm->device;
     return ncclSuccess;
 }
 

@@ -48,7 +48,8 @@ def test_c_caller(log_n, cols, log_lde, cap, threads, log_k):
     (13, 16, 3, 32, 2, 1),    # D = 8, k = 2 committed (proof.json's ratio): every block of k cosets
 ])
 def test_c_caller_collective_over_rccl_api(log_n, cols, log_lde, cap, threads, log_k):
-    """The collective commit through the library's RCCL code path at G = 2, 4, 8 ranks on one GPU:
+    """The collective commit through the library's RCCL code path at G = 2, 4, 8 ranks on one GPU
+    (and the world check each N > 1 bench line carries: counts, ranks, duplicated device):
     the mock librccl.so.1 (tests/c/mock_rccl.cpp) gives RCCL's semantics for in-process ranks, so
     the in-place ncclAllGather offsets, the grouped ncclSend / ncclRecv pairing and their stream
     ordering are exercised as a multi-GPU run issues them; results checked against the oracle."""
@@ -60,6 +61,9 @@ def test_c_caller_collective_over_rccl_api(log_n, cols, log_lde, cap, threads, l
                        capture_output=True, text=True, timeout=180, env=dict(os.environ, BJ_TEST_MOCK_RCCL=mock))
     assert r.returncode == 0, r.stdout + r.stderr
     assert "c_caller ok (collective also over RCCL's API" in r.stdout, r.stdout
+    # bj_comm_info / bj_comm_check_world through RCCL's API: ncclCommCount = 2, 4, 8 and each
+    # rank's ncclCommUserRank; the stand-in's ranks share one GPU and the check must say so
+    assert "rccl world check ok at world 2 4 8" in r.stdout, r.stdout
 
 
 @pytest.mark.gpu

@@ -88,3 +88,24 @@ def test_exchange_rejects_bad_arguments(pg):
             _exchange(comm, 0, a, a, 12)
     finally:
         comm.close()
+
+
+@pytest.mark.parametrize("make", ["world1", "process_group"])
+def test_rccl_comm_info_and_world_check(pg, make):
+    """bj_comm_info on the real RCCL: ncclCommCount 1, ncclCommUserRank 0, ncclCommCuDevice the
+    current device (torch's), its PCI bus id; bj_comm_check_world accepts the one-rank world.
+    The N > 1 bench line carries every rank's record from the same call."""
+    torch = pg
+    from boojum_amd.sharded import NativeComm
+    comm = NativeComm.rccl_world1() if make == "world1" else NativeComm.rccl()
+    try:
+        info = comm.info()
+        assert info["kind"] == "rccl"
+        assert (info["world"], info["rank"], info["transport_count"], info["transport_rank"]) == (1, 0, 1, 0)
+        assert info["device"] == torch.cuda.current_device()
+        assert info["pci_bus_id"] and info["host"]
+        ok, infos, msg = comm.check_world(torch.cuda.current_stream().cuda_stream)
+        assert ok, msg
+        assert infos == [info]
+    finally:
+        comm.close()
