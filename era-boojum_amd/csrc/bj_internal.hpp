@@ -98,13 +98,10 @@ hipError_t launch_lde3_table(uint64_t* out, uint32_t log_n, uint64_t shift, hipS
 // i (table tabs + i * tab_stride) of column c at lde + c * col_stride + i * coset_stride; with
 // log_k < log2(n_cosets) the cosets come in blocks of 2^log_k, coset i at
 // lde + c * col_stride + (i >> log_k) * block_stride + (i mod 2^log_k) * coset_stride.
-// parts: LDE3_MID and / or LDE3_FINAL (the final pass of cosets [0, n_cosets) alone reads the
-// middle pass's output in place: src, mono and inv_tab are then unused).
-constexpr uint32_t LDE3_MID = 1, LDE3_FINAL = 2;
 hipError_t launch_lde3(uint64_t* lde, size_t col_stride, size_t coset_stride, uint32_t n_cosets, const uint64_t* src,
                        size_t src_stride, uint64_t* mono, size_t mono_stride, uint32_t n_cols, uint32_t log_n,
                        const uint64_t* inv_tab, const uint64_t* tabs, size_t tab_stride, hipStream_t st,
-                       uint32_t log_k = 31, size_t block_stride = 0, uint32_t parts = LDE3_MID | LDE3_FINAL);
+                       uint32_t log_k = 31, size_t block_stride = 0);
 // the inverse tail on the inverse head's output src, folded by F = 2^log_f (1..3) for `shards`
 // targets: dst + P * dst_shard_stride + c * dst_col_stride receives column c's monomials folded
 // with s_pow_m[P] (launch_fold_all's output), the monomials themselves never written

@@ -154,11 +154,12 @@ def run_local(torch, world, n_cols, log_n, log_lde, cap, hasher, log_k=None):
     # G = 2 D in the three-pass range: half a coset per rank, the sender's fold
     (8, (16, 18, 2, 16, "poseidon2")),
     (8, (8, 19, 2, 4, "blake2s")),
-    # the inverse tail folding from registers (ntt_lde3.hip lde3_inv_kernel) at F = 4 and 8, and
-    # over B = 2 blocks of cosets (targets j G + p)
-    (8, (16, 18, 1, 16, "poseidon2")),        # F = 4
-    (8, (16, 18, 1, 16, "poseidon2", 0)),     # F = 8, B = 2
-    (8, (16, 18, 3, 32, "poseidon2", 2)),     # F = 2, B = 2
+    # the inverse tail folding from registers (ntt_lde3.hip lde3_inv_fold_kernel; G > D only) at
+    # F = G / k = 4 and 8, and over B = D / k = 2 blocks of cosets (targets j G + p)
+    (8, (16, 18, 1, 16, "poseidon2")),        # D = k = 2: F = 4, B = 1
+    (8, (16, 18, 1, 16, "poseidon2", 0)),     # D = 2, k = 1: F = 8, B = 2
+    (8, (16, 18, 2, 16, "poseidon2", 1)),     # D = 4, k = 2: F = 4, B = 2
+    (8, (16, 18, 3, 32, "poseidon2", 2)),     # G = D = 8, k = 4: the all-gather path (no fold), B = 2
     # G <= D in the three-pass range: the monomials all-gathered, whole cosets per rank
     (2, (16, 18, 2, 16, "poseidon2")),
     (4, (16, 18, 2, 16, "poseidon2")),        # one coset per rank
