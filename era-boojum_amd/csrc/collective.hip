@@ -159,8 +159,6 @@ struct bj_comm {
     int host_staged = 1;
     hipStream_t xs = nullptr;  // exchange stream, high priority, created on first use
     int xs_dev = -1;
-    hipStream_t ls = nullptr;  // leaf stream (column pipeline, K > 1 chunks), created on first use
-    int ls_dev = -1;
     // bj_comm_set_timing: (start, end, phase) event triples of the calls not yet read
     bool timing = false;
     struct Interval {
@@ -239,32 +237,6 @@ int exchange_stream(bj_comm* c, hipStream_t* out) {
     }
     *out = c->xs;
     return BJ_OK;
-}
-
-// The column pipeline's leaf stream: chunk k's leaves run there while the compute stream goes on
-// to chunk k + 1's LDE, so the LDE's blocks take the CUs a leaf grid's last round leaves idle
-// (a rank's leaf launches are short at G = 8: 10.7 rounds of the machine each).  Lowest priority:
-// when both have work queued, the LDE (which the next leaves wait for) is dispatched first.
-int leaf_stream(bj_comm* c, hipStream_t* out) {
-    int dev = 0;
-    HIP_CHECK(hipGetDevice(&dev), "hipGetDevice");
-    if (c->ls && c->ls_dev != dev) return err(BJ_EINVAL, "communicator used from another device");
-    if (!c->ls) {
-        int least = 0, greatest = 0;
-        HIP_CHECK(hipDeviceGetStreamPriorityRange(&least, &greatest), "stream priority range");
-        HIP_CHECK(hipStreamCreateWithPriority(&c->ls, hipStreamNonBlocking, least), "hipStreamCreate");
-        c->ls_dev = dev;
-    }
-    *out = c->ls;
-    return BJ_OK;
-}
-
-bool leaf_stream_enabled() {
-    static const bool on = [] {
-        const char* e = getenv("BJ_LEAF_STREAM");
-        return !(e && e[0] == '0');
-    }();
-    return on;
 }
 
 // recv block p <- rank p's send block (all-to-all: its block `rank`; all-gather: its only one)
@@ -697,7 +669,6 @@ int bj_comm_destroy(bj_comm* c) {
     }
     int rc = BJ_OK;
     if (c->xs) (void)hipStreamDestroy(c->xs);
-    if (c->ls) (void)hipStreamDestroy(c->ls);
     if (c->kind == bj_comm::RCCL_OWNED && c->nccl) {
         const Rccl& R = rccl();
         ncclResult_t e = R.destroy(c->nccl);
@@ -776,15 +747,9 @@ int bj_sharded_commit_d(bj_comm* comm, const uint64_t* trace_shard, size_t trace
         HIP_CHECK(arrived.make(K), "hipEventCreate");
     }
     std::vector<uint64_t> spm((size_t)B * world);
-    // the leaves of chunk k on their own stream, beside chunk k + 1's LDE (leaf_stream)
-    hipStream_t lst = st;
-    if (K > 1 && leaf_stream_enabled()) BJ_CHECK(leaf_stream(comm, &lst));
-    Events lde_done;
-    if (lst != st) HIP_CHECK(lde_done.make(K + 1), "hipEventCreate");
-    XsJoin ls_join(st, lst != st ? lst : nullptr);
     // phases 0 inverse (+ fold), 1 lde, 2 leaves, 3 nodes (bj_comm_set_timing)
     if (!comm->intervals.empty()) fold_intervals(comm, false);
-    PhaseTimer pt(comm, st), plt(comm, lst);
+    PhaseTimer pt(comm, st);
 
     // 1. local inverse transforms (and folds), each chunk's exchange issued as soon as its
     //    part is ready
@@ -861,24 +826,15 @@ int bj_sharded_commit_d(bj_comm* comm, const uint64_t* trace_shard, size_t trace
             const bool last = k + 1 == K;
             const uint64_t* cin = k == 0 ? nullptr : state;
             uint64_t* dst = last ? leaves : state;
-            if (lst != st) {
-                HIP_CHECK(hipEventRecord(lde_done.ev[k], st), "hipEventRecord");
-                HIP_CHECK(hipStreamWaitEvent(lst, lde_done.ev[k], 0), "hipStreamWaitEvent");
-            }
-            BJ_CHECK(plt.begin(2));
+            BJ_CHECK(pt.begin(2));
             if (hasher == BJ_HASHER_POSEIDON2)
-                BJ_CHECK(bj_merkle_leaves_partial_d(out, cc, m, m, cin, dst, last ? 1 : 0, lst));
+                BJ_CHECK(bj_merkle_leaves_partial_d(out, cc, m, m, cin, dst, last ? 1 : 0, st));
             else if (hasher == BJ_HASHER_BLAKE2S)
-                BJ_CHECK(bj_blake2s_leaves_partial_d(out, cc, m, m, r.c0, cin, dst, last ? 1 : 0, lst));
+                BJ_CHECK(bj_blake2s_leaves_partial_d(out, cc, m, m, r.c0, cin, dst, last ? 1 : 0, st));
             else
-                BJ_CHECK(bj_keccak256_leaves_d(out, cc, m, m, dst, lst));
-            BJ_CHECK(plt.end());
+                BJ_CHECK(bj_keccak256_leaves_d(out, cc, m, m, dst, st));
+            BJ_CHECK(pt.end());
         }
-    }
-    if (lst != st) {
-        // the compute stream takes the leaves back before the subtree (and the workspace's frees)
-        HIP_CHECK(hipEventRecord(lde_done.ev[K], lst), "hipEventRecord");
-        HIP_CHECK(hipStreamWaitEvent(st, lde_done.ev[K], 0), "hipStreamWaitEvent");
     }
     // 3. this rank's subtree, then the cap
     BJ_CHECK(pt.begin(3));
@@ -899,7 +855,7 @@ int bj_sharded_commit_d(bj_comm* comm, const uint64_t* trace_shard, size_t trace
                   "memcpy cap");
     }
     if (comm->timing) comm->timed_calls++;
-    xs_join.ok = ls_join.ok = abort_guard.ok = true;
+    xs_join.ok = abort_guard.ok = true;
     return BJ_OK;
 }
 
