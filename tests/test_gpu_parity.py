@@ -514,7 +514,7 @@ def test_release_workspace_between_host_commits(bj):
     commit re-allocates its workspace and is still bit-exact."""
     import ctypes
     from boojum_amd._lib import call, load
-    assert load().bj_abi_version() == (2 << 16) | 4
+    assert load().bj_abi_version() == (2 << 16) | 5
     c, log_n, log_d, cap = 40, 14, 2, 16
     tr = O.synthetic_trace(c, log_n)
     ref = O.lde_commit(tr, log_d, cap, threads=8)
