@@ -75,3 +75,20 @@ def test_rank_watchdog_under_an_external_launcher():
                        capture_output=True, text=True, timeout=120)
     assert r.returncode == 124 and "deadline passed in phase 'test-hang'" in r.stderr
     assert time.time() - t0 < 60
+
+
+def test_world_record_from_gathered_infos():
+    """The N > 1 line's transport record (bench.world_record) from bj_comm_check_world's gathered
+    bj_comm_info_t records: RCCL's own count and ranks, devices, bus ids, hosts."""
+    import bench
+    infos = [{"kind": "rccl", "world": 4, "rank": r, "transport_count": 4, "transport_rank": r, "device": r,
+              "pci_bus_id": "0000:%02x:00.0" % (0x10 * (r + 1)), "host": "node0"} for r in range(4)]
+    rec = bench.world_record(infos, "nccl", "")
+    assert rec["backend"] == "rccl" and rec["count"] == 4 and rec["ranks"] == [0, 1, 2, 3]
+    assert rec["devices"] == [0, 1, 2, 3] and rec["distinct_devices"] == 4 and rec["check"] == "ok"
+    assert rec["hosts"] == ["node0"]
+    # ranks that share a device (as the gloo rehearsal's do) count once; a failed check keeps its message
+    shared = [dict(i, device=0, pci_bus_id="0000:10:00.0") for i in infos]
+    rec = bench.world_record(shared, "gloo", "ranks 0 and 1 share device 0")
+    assert rec["backend"] == "gloo (callback transport)" and rec["distinct_devices"] == 1
+    assert rec["check"] == "ranks 0 and 1 share device 0"
