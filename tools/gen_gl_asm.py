@@ -531,7 +531,7 @@ def main():
     global LAYER_A_CHAINS, LAYER_B_CHAINS
     ap = argparse.ArgumentParser()
     ap.add_argument("--out", default=OUT, help="output header (variants for A/B builds elsewhere)")
-    ap.add_argument("--a-chains", type=int, default=LAYER_A_CHAINS, choices=(1, 2, 3, 4))
+    ap.add_argument("--a-chains", type=int, default=LAYER_A_CHAINS, choices=(1, 2, 3))  # L sums in v0..v5, H in v6..v11
     ap.add_argument("--b-chains", type=int, default=LAYER_B_CHAINS, choices=(1, 2))
     args = ap.parse_args()
     LAYER_A_CHAINS, LAYER_B_CHAINS = args.a_chains, args.b_chains
