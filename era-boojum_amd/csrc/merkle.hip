@@ -51,7 +51,10 @@ __device__ __forceinline__ void load8(p2::State& s, const uint64_t* q, size_t st
 // (the Overwrite sponge's rate words are overwritten by the next absorption, so the
 // capacity is the whole carried state between 8-element groups).  FINAL: write the digest
 // state[0..4]; otherwise write the capacity state[8..12] for the next column range.
-template <bool HAS_IN, bool FINAL>
+// REM: n_cols is not a multiple of 8 (a zero-padded last group); without it the kernel carries no
+// code, registers or branches for that case (C3's 256 columns, every 8-column chunk of the
+// collective's pipeline), and a FINAL absorption's last permutation is always the digest form.
+template <bool HAS_IN, bool FINAL, bool REM>
 __device__ __forceinline__ void leaf_hash_body(const uint64_t* __restrict__ src, size_t col_stride, uint32_t n_cols,
                                                size_t n_leaves, const uint64_t* cap_in, uint64_t* out) {
     const size_t L = blockIdx.x * (size_t)LEAF_THREADS + threadIdx.x;
@@ -69,7 +72,7 @@ __device__ __forceinline__ void leaf_hash_body(const uint64_t* __restrict__ src,
         }
     }
     const uint32_t full = n_cols >> 3;
-    const uint32_t rem = n_cols & 7;
+    const uint32_t rem = REM ? n_cols & 7 : 0;
     // software prefetch: the next group's 8 loads are issued before this group's permute
     uint64_t nxt[8];
     if (full > 0) {
@@ -96,12 +99,12 @@ __device__ __forceinline__ void leaf_hash_body(const uint64_t* __restrict__ src,
             s.lo[i] = (uint32_t)nxt[i];
             s.hi[i] = (uint32_t)(nxt[i] >> 32);
         }
-        if (FINAL && rem == 0)
+        if (FINAL && !REM)
             p2::permute<p2::OUT_DIGEST>(s);
         else
             p2::permute<p2::OUT_CAP>(s);
     }
-    if (FINAL && rem) {
+    if (FINAL && REM) {
         load8(s, p + (size_t)full * 8 * col_stride, col_stride, rem);
         p2::permute<p2::OUT_DIGEST>(s);
     }
@@ -109,14 +112,16 @@ __device__ __forceinline__ void leaf_hash_body(const uint64_t* __restrict__ src,
     else store_canon4_at(s, 2, out + 4 * L);
 }
 
-// Three waves per SIMD (<= 168 VGPRs) is what keeps the permutation at its issue rate: the
-// compiler's own allocation of the peeled absorptions would otherwise take 173 and drop to two.
-template <bool HAS_IN, bool FINAL>
-__global__ __launch_bounds__(LEAF_THREADS) __attribute__((amdgpu_waves_per_eu(3, 3))) void leaf_hash_kernel(const uint64_t* __restrict__ src,
+// Three waves per SIMD (<= 168 VGPRs) is what keeps the permutation at its issue rate.  Without
+// the ragged-group code (REM) every instantiation fits in 131-141 VGPRs on its own; a forced
+// amdgpu_waves_per_eu(3, 3) made the compiler serialise each full round's two constant loads
+// (one SGPR window for both), 0.4% of the leaves.
+template <bool HAS_IN, bool FINAL, bool REM>
+__global__ __launch_bounds__(LEAF_THREADS) void leaf_hash_kernel(const uint64_t* __restrict__ src,
                                                                  size_t col_stride, uint32_t n_cols,
                                                                  size_t n_leaves, const uint64_t* cap_in,
                                                                  uint64_t* out) {
-    leaf_hash_body<HAS_IN, FINAL>(src, col_stride, n_cols, n_leaves, cap_in, out);
+    leaf_hash_body<HAS_IN, FINAL, REM>(src, col_stride, n_cols, n_leaves, cap_in, out);
 }
 
 // Leaf hashing of MerkleTreeWithCap::construct_by_chunking (merkle_tree.rs:176-306) and
@@ -265,16 +270,24 @@ hipError_t launch_leaves_partial(const uint64_t* src, size_t col_stride, uint32_
                                  const uint64_t* cap_in, uint64_t* out, bool final_, hipStream_t st) {
     if (n_leaves == 0) return hipSuccess;
     const dim3 g((unsigned)((n_leaves + LEAF_THREADS - 1) / LEAF_THREADS));
-#define BJ_LEAF(IN, FIN) \
-    hipLaunchKernelGGL((leaf_hash_kernel<IN, FIN>), g, dim3(LEAF_THREADS), 0, st, src, col_stride, n_cols, n_leaves, \
-                       cap_in, out)
+#define BJ_LEAF(IN, FIN, REM) \
+    hipLaunchKernelGGL((leaf_hash_kernel<IN, FIN, REM>), g, dim3(LEAF_THREADS), 0, st, src, col_stride, n_cols, \
+                       n_leaves, cap_in, out)
+#define BJ_LEAF_R(IN, FIN) \
+    do {                     \
+        if (n_cols & 7)      \
+            BJ_LEAF(IN, FIN, true); \
+        else                 \
+            BJ_LEAF(IN, FIN, false); \
+    } while (0)
     if (cap_in) {
-        if (final_) BJ_LEAF(true, true);
-        else BJ_LEAF(true, false);
+        if (final_) BJ_LEAF_R(true, true);
+        else BJ_LEAF_R(true, false);
     } else {
-        if (final_) BJ_LEAF(false, true);
-        else BJ_LEAF(false, false);
+        if (final_) BJ_LEAF_R(false, true);
+        else BJ_LEAF_R(false, false);
     }
+#undef BJ_LEAF_R
 #undef BJ_LEAF
     return hipGetLastError();
 }

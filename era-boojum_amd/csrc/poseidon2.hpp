@@ -115,7 +115,12 @@ static_assert(full_rcs_fit(), "a full-round constant is too large for the one-ad
 
 // The schedule's device tables: full words, and (value, 0) limb pairs for the asm layers.
 struct Sched {
-    uint64_t rcw[30][12];                   // RC_FLAT as 64-bit words (full rounds, RC_4[0])
+    // RC_FLAT as 64-bit words (full rounds, RC_4[0]), elements 0..7 and 8..11 in tables of their
+    // own: one 64-byte and one 32-byte scalar load per round, each from its own base, so both are
+    // in flight together (one table of 12 had the second load's address formed after the first
+    // load's wait)
+    uint64_t rcw8[30][8];
+    uint64_t rcw4[30][4];
     uint64_t k_lo[11], k_hi[11];
     uint64_t d_lo[10], d_hi[10];
     uint64_t rc26_w[12], rc26_lo[12], rc26_hi[12];
@@ -123,7 +128,7 @@ struct Sched {
 constexpr Sched make_sched() {
     Sched s{};
     for (int r = 0; r < 30; r++)
-        for (int i = 0; i < 12; i++) s.rcw[r][i] = RC_FLAT[r][i];
+        for (int i = 0; i < 12; i++) (i < 8 ? s.rcw8[r][i] : s.rcw4[r][i - 8]) = RC_FLAT[r][i];
     for (int q = 0; q < 11; q++) { s.k_lo[q] = sched::V.k[q] & 0xFFFFFFFFull; s.k_hi[q] = sched::V.k[q] >> 32; }
     for (int q = 0; q < 10; q++) { s.d_lo[q] = sched::V.d[q] & 0xFFFFFFFFull; s.d_hi[q] = sched::V.d[q] >> 32; }
     for (int i = 0; i < 12; i++) {
@@ -243,7 +248,7 @@ template <int OUT = OUT_ALL, bool RC = true>
 __device__ __forceinline__ void full_round(State& s, uint64_t* L, uint64_t* H, int r) {
     if constexpr (RC) {
 #pragma unroll
-        for (int i = 0; i < 12; i++) L[i] += SCH.rcw[r][i];
+        for (int i = 0; i < 12; i++) L[i] += i < 8 ? SCH.rcw8[r][i] : SCH.rcw4[r][i - 8];
     }
     reduce12(L, H, s.lo, s.hi);
 #pragma unroll
@@ -313,7 +318,7 @@ __device__ __forceinline__ void permute(State& s) {
     mds_ext_limbs(s.hi, H);
 #pragma unroll 1
     for (int r = 0; r < 4; r++) full_round(s, L, H, r);
-    L[0] += SCH.rcw[4][0];
+    L[0] += SCH.rcw8[4][0];
 #pragma unroll
     for (int q = 0; q < 3; q++) {
         const int i = 4 * q;
