@@ -13,7 +13,8 @@ import json
 import os
 import sys
 
-# PROBE_INTERFERE=1: also the same calls beside an exchange-shaped disturbance (interference())
+# PROBE_INTERFERE=1: also the same calls beside an exchange-shaped disturbance (interference());
+# PROBE_PHASE_EVENTS_TIMED=1 times those calls with the phase events on, as rounds 4-5 did
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, os.path.join(ROOT, "era-boojum_amd"))
@@ -29,25 +30,34 @@ def links(world):
     return min(world - 1, 7)
 
 
-def _timed(comm, tr, res, n_cols, log_n, log_lde, cap, reps):
-    """ms per call (events around it on the compute stream) and the phase split."""
+def _timed(comm, tr, res, n_cols, log_n, log_lde, cap, reps, phase_events_in_timed=False):
+    """ms per call (events around it on the compute stream) and the phase split.  The timed calls
+    run as a production call does, without the library's phase events (bj_comm_set_timing), and
+    the phase split comes from `reps` further calls with them on; phase_events_in_timed=True
+    times the calls that record the phases (round 4 and round 5's r5o tables were taken so)."""
     import torch
     from boojum_amd.sharded import native_sharded_commit
     native_sharded_commit(comm, tr, n_cols, log_n, log_lde, cap, out=res)  # warm-up
     torch.cuda.synchronize()
     comm.phase_ms()
-    comm.set_timing(True)
-    tot = 0.0
-    for _ in range(reps):
-        s, e = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-        s.record()
-        native_sharded_commit(comm, tr, n_cols, log_n, log_lde, cap, out=res)
-        e.record()
-        torch.cuda.synchronize()
-        tot += s.elapsed_time(e)
+
+    def run(timing):
+        comm.set_timing(timing)
+        tot = 0.0
+        for _ in range(reps):
+            s, e = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            s.record()
+            native_sharded_commit(comm, tr, n_cols, log_n, log_lde, cap, out=res)
+            e.record()
+            torch.cuda.synchronize()
+            tot += s.elapsed_time(e)
+        comm.set_timing(False)
+        return tot / reps
+
+    ms = None if phase_events_in_timed else run(False)
+    ms_ev = run(True)
     ph, calls = comm.phase_ms()
-    comm.set_timing(False)
-    return tot / reps, {k: v / max(1, calls) for k, v in ph.items()}
+    return (ms_ev if ms is None else ms), {k: v / max(1, calls) for k, v in ph.items()}
 
 
 def interference(comm0, tr, res, n_cols, log_n, log_lde, cap, world, recv, reps, ph0, calls0):
@@ -71,8 +81,10 @@ def interference(comm0, tr, res, n_cols, log_n, log_lde, cap, world, recv, reps,
     ring = 512 << 20  # a 512 MiB ring: past the 256 MiB Infinity Cache, so the bytes reach HBM
     a_buf = torch.empty(ring // 8, dtype=torch.int64, device="cuda")
     b_buf = torch.empty_like(a_buf)
-    base_ms, base_ph = _timed(comm0, tr, res, n_cols, log_n, log_lde, cap, reps)
-    rows = {"stubbed": {"ms": round(base_ms, 2), "phase_ms": {k: round(v, 2) for k, v in base_ph.items()}}}
+    ev = bool(os.environ.get("PROBE_PHASE_EVENTS_TIMED"))
+    base_ms, base_ph = _timed(comm0, tr, res, n_cols, log_n, log_lde, cap, reps, ev)
+    rows = {"phase_events_in_timed_calls": ev,
+            "stubbed": {"ms": round(base_ms, 2), "phase_ms": {k: round(v, 2) for k, v in base_ph.items()}}}
     shapes = [("burst_32ch", 32, 0.0)]
     for per_link in LINK_GBS:
         for ch in (8, 16, 32):
@@ -84,7 +96,7 @@ def interference(comm0, tr, res, n_cols, log_n, log_lde, cap, world, recv, reps,
         fn = EXCHANGE_FN(exchange)
         comm = NativeComm._make("bj_comm_init_callback", world, 0, fn, None, 0, world=world, rank=0, keep=fn)
         try:
-            ms, ph = _timed(comm, tr, res, n_cols, log_n, log_lde, cap, reps)
+            ms, ph = _timed(comm, tr, res, n_cols, log_n, log_lde, cap, reps, ev)
         finally:
             comm.close()
         rows[name] = {"ms": round(ms, 2), "delta_ms": round(ms - base_ms, 2),
