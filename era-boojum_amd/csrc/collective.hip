@@ -331,6 +331,17 @@ uint32_t log2u(uint64_t x) {
     return l;
 }
 
+// BJ_LEAVES_DEFER=d (experiments, tools/shard_compute_probe.py): chunk k's leaves are issued
+// after chunk k + d's LDE instead of right after its own (d = 0), so fewer LDE -> leaf switches
+// happen on the compute stream; larger d needs the later chunks' exchanges earlier.
+size_t leaves_defer() {
+    static const size_t v = [] {
+        const char* e = getenv("BJ_LEAVES_DEFER");
+        return e ? (size_t)strtoull(e, nullptr, 0) : (size_t)0;
+    }();
+    return v;
+}
+
 struct Run {
     uint32_t lo, global, count;  // local first row, global first column, columns
     uint32_t c0, c1;             // the chunk's global column range
@@ -800,7 +811,26 @@ int bj_sharded_commit_d(bj_comm* comm, const uint64_t* trace_shard, size_t trace
         }
     }
     // 2. per arrived chunk: this rank's part of the committed block (block 0) of its columns'
-    //    LDE, absorbed into the sponges, then its part of the other blocks (LDE only)
+    //    LDE, absorbed into the sponges, then its part of the other blocks (LDE only).  Chunk k's
+    //    leaves follow chunk k + defer's LDE (leaves_defer(); 0 in production).
+    auto absorb = [&](size_t k) -> int {
+        const Run& r = runs[k];
+        const uint32_t cc = r.c1 - r.c0;
+        const uint64_t* out = lde + (size_t)r.c0 * m;  // block 0
+        const bool last = k + 1 == K;
+        const uint64_t* cin = k == 0 ? nullptr : state;
+        uint64_t* dst = last ? leaves : state;
+        BJ_CHECK(pt.begin(2));
+        if (hasher == BJ_HASHER_POSEIDON2)
+            BJ_CHECK(bj_merkle_leaves_partial_d(out, cc, m, m, cin, dst, last ? 1 : 0, st));
+        else if (hasher == BJ_HASHER_BLAKE2S)
+            BJ_CHECK(bj_blake2s_leaves_partial_d(out, cc, m, m, r.c0, cin, dst, last ? 1 : 0, st));
+        else
+            BJ_CHECK(bj_keccak256_leaves_d(out, cc, m, m, dst, st));
+        return pt.end();
+    };
+    const size_t defer = leaves_defer();
+    size_t absorbed = 0;
     for (size_t k = 0; k < K; k++) {
         const Run& r = runs[k];
         const uint32_t cc = r.c1 - r.c0;
@@ -822,20 +852,11 @@ int bj_sharded_commit_d(bj_comm* comm, const uint64_t* trace_shard, size_t trace
             else
                 BJ_CHECK(bj_lde_shard_d(coeffs + (size_t)r.c0 * n, cc, n, log_n, log_lde, ls, shard, work, out, st));
             BJ_CHECK(pt.end());
-            if (j) continue;
-            const bool last = k + 1 == K;
-            const uint64_t* cin = k == 0 ? nullptr : state;
-            uint64_t* dst = last ? leaves : state;
-            BJ_CHECK(pt.begin(2));
-            if (hasher == BJ_HASHER_POSEIDON2)
-                BJ_CHECK(bj_merkle_leaves_partial_d(out, cc, m, m, cin, dst, last ? 1 : 0, st));
-            else if (hasher == BJ_HASHER_BLAKE2S)
-                BJ_CHECK(bj_blake2s_leaves_partial_d(out, cc, m, m, r.c0, cin, dst, last ? 1 : 0, st));
-            else
-                BJ_CHECK(bj_keccak256_leaves_d(out, cc, m, m, dst, st));
-            BJ_CHECK(pt.end());
+            if (j == 0)
+                while (absorbed + defer <= k) BJ_CHECK(absorb(absorbed++));
         }
     }
+    while (absorbed < K) BJ_CHECK(absorb(absorbed++));
     // 3. this rank's subtree, then the cap
     BJ_CHECK(pt.begin(3));
     BJ_CHECK(nodes_for(hasher, leaves, m, cap_local, nodes, st));
