@@ -342,18 +342,6 @@ size_t leaves_defer() {
     return v;
 }
 
-// BJ_XCHG_HOLD=h (experiments, tools/shard_compute_probe.py PROBE_INTERFERE=1): 1 issues every
-// chunk's exchange only after the last chunk's inverse (+ fold), 2 all but the first, so the
-// exchanges stop sharing the machine with the inverse phase; 0 issues each as soon as its chunk
-// is ready.
-int xchg_hold() {
-    static const int v = [] {
-        const char* e = getenv("BJ_XCHG_HOLD");
-        return e ? atoi(e) : 0;
-    }();
-    return v;
-}
-
 struct Run {
     uint32_t lo, global, count;  // local first row, global first column, columns
     uint32_t c0, c1;             // the chunk's global column range
@@ -775,26 +763,11 @@ int bj_sharded_commit_d(bj_comm* comm, const uint64_t* trace_shard, size_t trace
     PhaseTimer pt(comm, st);
 
     // 1. local inverse transforms (and folds), each chunk's exchange issued as soon as its
-    //    part is ready (xchg_hold() holds some back until every inverse is done; 0 in production)
-    const int hold = xchg_hold();
-    auto held = [&](size_t k) { return hold == 1 || (hold == 2 && k > 0); };
-    auto exchange = [&](size_t k) -> int {
-        const Run& r = runs[k];
-        if (fold) {
-            const uint64_t* snd = send + (size_t)world * B * m * r.lo;
-            for (uint32_t j = 0; j < B; j++)
-                BJ_CHECK(all_to_all(comm, snd + (size_t)j * world * r.count * m,
-                                    folded + ((size_t)j * n_cols + r.c0) * m, (size_t)r.count * m * 8, xs));
-        } else {
-            BJ_CHECK(all_gather(comm, coeffs + (size_t)r.global * n, coeffs + (size_t)r.c0 * n,
-                                (size_t)r.count * n * 8, xs));
-        }
-        HIP_CHECK(hipEventRecord(arrived.ev[k], xs), "hipEventRecord");
-        return BJ_OK;
-    };
+    //    part is ready
     for (size_t k = 0; k < K; k++) {
         const Run& r = runs[k];
         const uint64_t* tr = trace_shard + (size_t)r.lo * trace_stride;
+        hipStream_t xst = world > 1 ? xs : st;
         if (fold) {
             // send layout per run: [block j][rank p][c][m], so block j's all-to-all is contiguous
             uint64_t* snd = send + (size_t)world * B * m * r.lo;
@@ -815,25 +788,27 @@ int bj_sharded_commit_d(bj_comm* comm, const uint64_t* trace_shard, size_t trace
                               "fold");
             }
             BJ_CHECK(pt.end());
+            if (world > 1) {
+                HIP_CHECK(hipEventRecord(in.ev[k], st), "hipEventRecord");
+                HIP_CHECK(hipStreamWaitEvent(xs, in.ev[k], 0), "hipStreamWaitEvent");
+            }
+            for (uint32_t j = 0; j < B; j++)
+                BJ_CHECK(all_to_all(comm, snd + (size_t)j * world * r.count * m,
+                                    folded + ((size_t)j * n_cols + r.c0) * m, (size_t)r.count * m * 8, xst));
+            if (world > 1) HIP_CHECK(hipEventRecord(arrived.ev[k], xs), "hipEventRecord");
         } else {
             if (fused) continue;  // the inverse runs inside the fused LDE (step 2)
             uint64_t* mine = coeffs + (size_t)r.global * n;
             BJ_CHECK(pt.begin(0));
             BJ_CHECK(bj_lde_coeffs_d(tr, r.count, trace_stride, log_n, mine, n, st));
             BJ_CHECK(pt.end());
-        }
-        if (world > 1) {  // (fold implies world > 1)
-            HIP_CHECK(hipEventRecord(in.ev[k], st), "hipEventRecord");
-            if (!held(k)) {
+            if (world > 1) {
+                HIP_CHECK(hipEventRecord(in.ev[k], st), "hipEventRecord");
                 HIP_CHECK(hipStreamWaitEvent(xs, in.ev[k], 0), "hipStreamWaitEvent");
-                BJ_CHECK(exchange(k));
+                BJ_CHECK(all_gather(comm, mine, coeffs + (size_t)r.c0 * n, (size_t)r.count * n * 8, xs));
+                HIP_CHECK(hipEventRecord(arrived.ev[k], xs), "hipEventRecord");
             }
         }
-    }
-    if (world > 1 && hold) {
-        HIP_CHECK(hipStreamWaitEvent(xs, in.ev[K - 1], 0), "hipStreamWaitEvent");
-        for (size_t k = 0; k < K; k++)
-            if (held(k)) BJ_CHECK(exchange(k));
     }
     // 2. per arrived chunk: this rank's part of the committed block (block 0) of its columns'
     //    LDE, absorbed into the sponges, then its part of the other blocks (LDE only).  Chunk k's
