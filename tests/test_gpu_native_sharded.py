@@ -449,3 +449,32 @@ def test_local_exchange_layouts():
         for p in range(world):
             assert torch.equal(ag[p * m:(p + 1) * m], i + 10**6 * p)
             assert torch.equal(a2a[p * m:(p + 1) * m], i + 10**6 * p + 10**3 * P)
+
+
+@pytest.mark.parametrize("defer", [1, 99])
+def test_native_sharded_commit_leaves_deferred(torch_mod, defer):
+    """BJ_LEAVES_DEFER (collective.hip leaves_defer(), read once per process): chunk k's leaves
+    after chunk k + d's LDE, or after every LDE, must give the same commitment.  Run in a child
+    process, since the knob is read once."""
+    import os
+    import subprocess
+    import sys
+    here = os.path.dirname(os.path.abspath(__file__))
+    code = "\n".join([
+        # conftest.py's path order: oracle/ (oracle.py), the package, the repo root, then tests/
+        "import sys; sys.path[:0] = [%r, %r, %r, %r]" % (os.path.join(os.path.dirname(here), "oracle"),
+                                                        os.path.join(os.path.dirname(here), "era-boojum_amd"),
+                                                        os.path.dirname(here), here),
+        "import torch, boojum_amd; boojum_amd.load()",
+        "import test_gpu_native_sharded as T",
+        "for world, cfg in [(8, (256, 13, 2, 16, 'poseidon2')), (2, (16, 18, 2, 16, 'poseidon2')),",
+        "                   (4, (16, 13, 1, 16, 'poseidon2')), (2, (16, 13, 2, 16, 'blake2s'))]:",
+        "    outs = T.run_local(torch, world, *cfg)",
+        "    ref = T.reference(*cfg)",
+        "    for P in range(world):",
+        "        T.check_rank(ref, P, world, cfg[3], *outs[P], hasher=cfg[4])",
+        "print('deferred leaves ok')",
+    ])
+    env = dict(os.environ, BJ_LEAVES_DEFER=str(defer))
+    r = subprocess.run([sys.executable, "-c", code], env=env, capture_output=True, text=True, timeout=240)
+    assert r.returncode == 0 and "deferred leaves ok" in r.stdout, r.stdout[-2000:] + r.stderr[-4000:]
