@@ -373,8 +373,14 @@ __global__ __launch_bounds__(NT, 2) void lde3_inv_fold_kernel(const uint64_t* sr
                                                               const uint64_t* __restrict__ inv_tab, InvFoldZ zc) {
     __shared__ uint64_t lds[PAD_LDS];
     const uint32_t t = threadIdx.x;
-    const uint32_t c = __builtin_amdgcn_readfirstlane(blockIdx.x % n_cols);
-    const uint32_t q = __builtin_amdgcn_readfirstlane(blockIdx.x / n_cols);
+    // columns fastest, XCD-aware (as the final pass): blocks are dealt round-robin over the 8
+    // XCDs, so the n_cols blocks of one q (the same inverse-tail factor slices, ~67 KB) sit at ids
+    // 8 (q8 n_cols + c) + (q & 7), all on one XCD, and the slices reach that XCD's L2 once instead
+    // of once per XCD (C3 at G = 8: 0.82 GB of factor reads per rank call with q spread over the
+    // XCDs, profiles/r5zi_shard_pmc_summary.txt); 2^R, the number of q, is a multiple of 8
+    const uint32_t rest = blockIdx.x >> 3;
+    const uint32_t c = __builtin_amdgcn_readfirstlane(rest % n_cols);
+    const uint32_t q = __builtin_amdgcn_readfirstlane(((rest / n_cols) << 3) | (blockIdx.x & 7));
     uint64_t x[PT];
     {
         const auto rb = uniform_rsrc(src + (size_t)c * src_stride + (size_t)q * TILE, 8u * TILE);
