@@ -366,10 +366,33 @@ struct InvFoldZ {
     uint64_t z[kInvFoldConsts];  // z[P F + bitrev_F(a)] = (s_P^m)^a
 };
 
+// Target P's OUTS outputs of this thread (block positions OUTS t + i) out through LDS half P & 1,
+// coalesced: one barrier per target (the other half's reads, a target earlier, are behind it).
+template <uint32_t OUTS>
+__device__ __forceinline__ void store_fold_target(const uint64_t* h, uint64_t* lds, uint32_t P, uint32_t t, uint64_t* dst,
+                                                  size_t dst_col_stride, size_t dst_shard_stride, uint32_t c,
+                                                  uint32_t q) {
+    constexpr uint32_t BLK = NT * OUTS, HALF = PAD_LDS / 2;
+    uint64_t* buf = lds + (P & 1) * HALF;
+#pragma unroll
+    for (uint32_t i = 0; i < OUTS; i++) {
+        const uint32_t w = OUTS * t + i;
+        buf[w + (w >> 5)] = h[i];
+    }
+    __syncthreads();
+    const auto rs = uniform_rsrc(dst + (size_t)P * dst_shard_stride + (size_t)c * dst_col_stride + (size_t)q * BLK,
+                                 8u * BLK);
+#pragma unroll
+    for (uint32_t k = 0; k < OUTS; k++) {
+        const uint32_t w = t + NT * k;
+        __builtin_amdgcn_raw_buffer_store_b64(as_u32x2(buf[w + (w >> 5)]), rs, (int)(t * 8), (int)(k * 2048), 0);
+    }
+}
+
 template <int R, int LOG_F>
 __global__ __launch_bounds__(NT, 2) void lde3_inv_fold_kernel(const uint64_t* src, size_t src_stride, uint64_t* dst,
                                                               size_t dst_col_stride, size_t dst_shard_stride,
-                                                              uint32_t n_cols, uint32_t shards,
+                                                              uint32_t n_cols, uint32_t shards, uint32_t paired,
                                                               const uint64_t* __restrict__ inv_tab, InvFoldZ zc) {
     __shared__ uint64_t lds[PAD_LDS];
     const uint32_t t = threadIdx.x;
@@ -394,6 +417,35 @@ __global__ __launch_bounds__(NT, 2) void lde3_inv_fold_kernel(const uint64_t* sr
         constexpr uint32_t F = 1u << LOG_F, OUTS = PT / F, BLK = TILE / F, HALF = PAD_LDS / 2;
         static_assert(OUTS % 4 == 0 && BLK + BLK / 32 <= HALF, "fold layout");
         __syncthreads();  // the tail's last LDS reads are done before the halves are written
+        if constexpr (LOG_F == 1) {
+            if (paired) {
+                // targets 2P' and 2P' + 1 fold with z and -z (the two halves of one coset: s_P^m and
+                // (s_P w_n)^m = -s_P^m), so each output pair is one CT butterfly, (c0 + z c1,
+                // c0 - z c1): 26 instructions where two products and two sums took 44
+#pragma unroll 1
+                for (uint32_t P = 0; P < shards; P += 2) {
+                    const uint64_t z = zc.z[P * F + 1];
+                    uint64_t h0[OUTS], h1[OUTS];
+#pragma unroll
+                    for (uint32_t i = 0; i < OUTS; i++) {
+                        h0[i] = x[2 * i];
+                        h1[i] = x[2 * i + 1];
+                    }
+#pragma unroll
+                    for (uint32_t i = 0; i < OUTS; i += 4)
+                        ct_bfly_x4(h0[i], h1[i], h0[i + 1], h1[i + 1], h0[i + 2], h1[i + 2], h0[i + 3], h1[i + 3], z,
+                                   z, z, z);
+#pragma unroll
+                    for (uint32_t i = 0; i < OUTS; i += 4) {
+                        canon4(h0 + i);
+                        canon4(h1 + i);
+                    }
+                    store_fold_target<OUTS>(h0, lds, P, t, dst, dst_col_stride, dst_shard_stride, c, q);
+                    store_fold_target<OUTS>(h1, lds, P + 1, t, dst, dst_col_stride, dst_shard_stride, c, q);
+                }
+                return;
+            }
+        }
 #pragma unroll 1
         for (uint32_t P = 0; P < shards; P++) {
             uint64_t h[OUTS];
@@ -421,22 +473,7 @@ __global__ __launch_bounds__(NT, 2) void lde3_inv_fold_kernel(const uint64_t* sr
             }
 #pragma unroll
             for (uint32_t i = 0; i < OUTS; i += 4) canon4(h + i);
-            uint64_t* buf = lds + (P & 1) * HALF;
-#pragma unroll
-            for (uint32_t i = 0; i < OUTS; i++) {
-                const uint32_t w = OUTS * t + i;
-                buf[w + (w >> 5)] = h[i];
-            }
-            __syncthreads();
-            const auto rs = uniform_rsrc(dst + (size_t)P * dst_shard_stride + (size_t)c * dst_col_stride +
-                                             (size_t)q * BLK,
-                                         8u * BLK);
-#pragma unroll
-            for (uint32_t k = 0; k < OUTS; k++) {
-                const uint32_t w = t + NT * k;
-                __builtin_amdgcn_raw_buffer_store_b64(as_u32x2(buf[w + (w >> 5)]), rs, (int)(t * 8), (int)(k * 2048),
-                                                      0);
-            }
+            store_fold_target<OUTS>(h, lds, P, t, dst, dst_col_stride, dst_shard_stride, c, q);
         }
     }
 }
@@ -717,12 +754,12 @@ hipError_t launch_lde3(uint64_t* lde, size_t col_stride, size_t coset_stride, ui
 namespace {
 template <int R>
 void launch_lde3_inv_fold_R(uint64_t* dst, size_t dst_col_stride, size_t dst_shard_stride, const uint64_t* src,
-                            size_t src_stride, uint32_t n_cols, uint32_t log_f, uint32_t shards,
+                            size_t src_stride, uint32_t n_cols, uint32_t log_f, uint32_t shards, uint32_t paired,
                             const uint64_t* inv_tab, const InvFoldZ& zc, hipStream_t st) {
     const dim3 g(n_cols << R);
 #define BJ_INV(LF)                                                                                             \
     hipLaunchKernelGGL((lde3_inv_fold_kernel<R, LF>), g, dim3(NT), 0, st, src, src_stride, dst, dst_col_stride, \
-                       dst_shard_stride, n_cols, shards, inv_tab, zc)
+                       dst_shard_stride, n_cols, shards, paired, inv_tab, zc)
     switch (log_f) {
         case 1: BJ_INV(1); break;
         case 2: BJ_INV(2); break;
@@ -752,8 +789,14 @@ hipError_t launch_lde3_inv_fold(uint64_t* dst, size_t dst_col_stride, size_t dst
             acc = gl::mul(acc, s_pow_m[P]);
         }
     }
+    // F = 2 with targets in pairs (2P', 2P' + 1) whose s^m are negatives of each other (the
+    // collective's targets are: their shifts are s and s w_n): the butterfly form
+    uint32_t paired = log_f == 1 && shards % 2 == 0 && !getenv("BJ_INV_FOLD_UNPAIRED");
+    for (uint32_t P = 0; paired && P < shards; P += 2)
+        paired = gl::canon(s_pow_m[P + 1]) == gl::canon(gl::sub(0, s_pow_m[P]));
 #define BJ_INVR(RR) \
-    launch_lde3_inv_fold_R<RR>(dst, dst_col_stride, dst_shard_stride, src, src_stride, n_cols, log_f, shards, inv_tab, zc, st)
+    launch_lde3_inv_fold_R<RR>(dst, dst_col_stride, dst_shard_stride, src, src_stride, n_cols, log_f, shards, paired, \
+                               inv_tab, zc, st)
     switch (log_n - 13) {
         case 5: BJ_INVR(5); break;
         case 6: BJ_INVR(6); break;
