@@ -366,6 +366,49 @@ struct InvFoldZ {
     uint64_t z[kInvFoldConsts];  // z[P F + bitrev_F(a)] = (s_P^m)^a
 };
 
+// acc[i] (+)= x[F i + b] * zb for i < OUTS; with set, acc[i] = the product.
+template <uint32_t OUTS, uint32_t F>
+__device__ __forceinline__ void fold_term(uint64_t* acc, const uint64_t* x, uint32_t b, uint64_t zb, bool set) {
+    const uint32_t z0 = (uint32_t)zb, z1 = (uint32_t)(zb >> 32);
+#pragma unroll
+    for (uint32_t i = 0; i < OUTS; i += 4) {
+        uint32_t p0[4], p1[4], s0[4], s1[4];
+        glasm::mul_sb_x4((uint32_t)x[F * i + b], (uint32_t)(x[F * i + b] >> 32), z0, z1, p0[0], p1[0],
+                         (uint32_t)x[F * (i + 1) + b], (uint32_t)(x[F * (i + 1) + b] >> 32), z0, z1, p0[1], p1[1],
+                         (uint32_t)x[F * (i + 2) + b], (uint32_t)(x[F * (i + 2) + b] >> 32), z0, z1, p0[2], p1[2],
+                         (uint32_t)x[F * (i + 3) + b], (uint32_t)(x[F * (i + 3) + b] >> 32), z0, z1, p0[3], p1[3]);
+        if (set) {
+#pragma unroll
+            for (int j = 0; j < 4; j++) acc[i + j] = join2(p0[j], p1[j]);
+            continue;
+        }
+        glasm::add_x4((uint32_t)acc[i], (uint32_t)(acc[i] >> 32), p0[0], p1[0], s0[0], s1[0], (uint32_t)acc[i + 1],
+                      (uint32_t)(acc[i + 1] >> 32), p0[1], p1[1], s0[1], s1[1], (uint32_t)acc[i + 2],
+                      (uint32_t)(acc[i + 2] >> 32), p0[2], p1[2], s0[2], s1[2], (uint32_t)acc[i + 3],
+                      (uint32_t)(acc[i + 3] >> 32), p0[3], p1[3], s0[3], s1[3]);
+#pragma unroll
+        for (int j = 0; j < 4; j++) acc[i + j] = join2(s0[j], s1[j]);
+    }
+}
+
+// (a, b) <- (a + b, a - b) on four pairs (any u64 in and out)
+__device__ __forceinline__ void add_sub4(uint64_t* a, uint64_t* b) {
+    uint32_t s0[4], s1[4], d0[4], d1[4];
+    glasm::add_x4((uint32_t)a[0], (uint32_t)(a[0] >> 32), (uint32_t)b[0], (uint32_t)(b[0] >> 32), s0[0], s1[0],
+                  (uint32_t)a[1], (uint32_t)(a[1] >> 32), (uint32_t)b[1], (uint32_t)(b[1] >> 32), s0[1], s1[1],
+                  (uint32_t)a[2], (uint32_t)(a[2] >> 32), (uint32_t)b[2], (uint32_t)(b[2] >> 32), s0[2], s1[2],
+                  (uint32_t)a[3], (uint32_t)(a[3] >> 32), (uint32_t)b[3], (uint32_t)(b[3] >> 32), s0[3], s1[3]);
+    glasm::sub_x4((uint32_t)a[0], (uint32_t)(a[0] >> 32), (uint32_t)b[0], (uint32_t)(b[0] >> 32), d0[0], d1[0],
+                  (uint32_t)a[1], (uint32_t)(a[1] >> 32), (uint32_t)b[1], (uint32_t)(b[1] >> 32), d0[1], d1[1],
+                  (uint32_t)a[2], (uint32_t)(a[2] >> 32), (uint32_t)b[2], (uint32_t)(b[2] >> 32), d0[2], d1[2],
+                  (uint32_t)a[3], (uint32_t)(a[3] >> 32), (uint32_t)b[3], (uint32_t)(b[3] >> 32), d0[3], d1[3]);
+#pragma unroll
+    for (int j = 0; j < 4; j++) {
+        a[j] = join2(s0[j], s1[j]);
+        b[j] = join2(d0[j], d1[j]);
+    }
+}
+
 // Target P's OUTS outputs of this thread (block positions OUTS t + i) out through LDS half P & 1,
 // coalesced: one barrier per target (the other half's reads, a target earlier, are behind it).
 template <uint32_t OUTS>
@@ -417,15 +460,18 @@ __global__ __launch_bounds__(NT, 2) void lde3_inv_fold_kernel(const uint64_t* sr
         constexpr uint32_t F = 1u << LOG_F, OUTS = PT / F, BLK = TILE / F, HALF = PAD_LDS / 2;
         static_assert(OUTS % 4 == 0 && BLK + BLK / 32 <= HALF, "fold layout");
         __syncthreads();  // the tail's last LDS reads are done before the halves are written
-        if constexpr (LOG_F == 1) {
-            if (paired) {
-                // targets 2P' and 2P' + 1 fold with z and -z (the two halves of one coset: s_P^m and
-                // (s_P w_n)^m = -s_P^m), so each output pair is one CT butterfly, (c0 + z c1,
-                // c0 - z c1): 26 instructions where two products and two sums took 44
+        if (paired) {
+            // targets P and P + 1 (P even) fold with z and -z: their shifts s and s' differ by
+            // w^(2^(ls-1)), and (s'/s)^m = -1 (tests/test_fold_pairing.py).  Register b carries
+            // the exponent bitrev_F(b), odd exactly for b >= F/2, so with E = the even-exponent
+            // terms and O = the odd ones, target P gets E + O and target P + 1 gets E - O: half the
+            // products.  At F = 2 that is one CT butterfly per output pair, (c0 + z c1, c0 - z c1):
+            // 26 instructions where two products and two sums took 44.
 #pragma unroll 1
-                for (uint32_t P = 0; P < shards; P += 2) {
+            for (uint32_t P = 0; P < shards; P += 2) {
+                uint64_t h0[OUTS], h1[OUTS];
+                if constexpr (F == 2) {
                     const uint64_t z = zc.z[P * F + 1];
-                    uint64_t h0[OUTS], h1[OUTS];
 #pragma unroll
                     for (uint32_t i = 0; i < OUTS; i++) {
                         h0[i] = x[2 * i];
@@ -435,16 +481,31 @@ __global__ __launch_bounds__(NT, 2) void lde3_inv_fold_kernel(const uint64_t* sr
                     for (uint32_t i = 0; i < OUTS; i += 4)
                         ct_bfly_x4(h0[i], h1[i], h0[i + 1], h1[i + 1], h0[i + 2], h1[i + 2], h0[i + 3], h1[i + 3], z,
                                    z, z, z);
+                } else {
+                    uint64_t e[OUTS], o[OUTS];
 #pragma unroll
-                    for (uint32_t i = 0; i < OUTS; i += 4) {
-                        canon4(h0 + i);
-                        canon4(h1 + i);
-                    }
-                    store_fold_target<OUTS>(h0, lds, P, t, dst, dst_col_stride, dst_shard_stride, c, q);
-                    store_fold_target<OUTS>(h1, lds, P + 1, t, dst, dst_col_stride, dst_shard_stride, c, q);
+                    for (uint32_t i = 0; i < OUTS; i++) e[i] = x[F * i];
+#pragma unroll
+                    for (uint32_t b = 1; b < F; b++)
+                        fold_term<OUTS, F>(b < F / 2 ? e : o, x, b, zc.z[P * F + b], b == F / 2);
+#pragma unroll
+                    for (uint32_t i = 0; i < OUTS; i += 4)
+                        for (int j = 0; j < 4; j++) {
+                            h0[i + j] = e[i + j];
+                            h1[i + j] = o[i + j];
+                        }
+#pragma unroll
+                    for (uint32_t i = 0; i < OUTS; i += 4) add_sub4(h0 + i, h1 + i);
                 }
-                return;
+#pragma unroll
+                for (uint32_t i = 0; i < OUTS; i += 4) {
+                    canon4(h0 + i);
+                    canon4(h1 + i);
+                }
+                store_fold_target<OUTS>(h0, lds, P, t, dst, dst_col_stride, dst_shard_stride, c, q);
+                store_fold_target<OUTS>(h1, lds, P + 1, t, dst, dst_col_stride, dst_shard_stride, c, q);
             }
+            return;
         }
 #pragma unroll 1
         for (uint32_t P = 0; P < shards; P++) {
@@ -452,25 +513,7 @@ __global__ __launch_bounds__(NT, 2) void lde3_inv_fold_kernel(const uint64_t* sr
 #pragma unroll
             for (uint32_t i = 0; i < OUTS; i++) h[i] = x[F * i];
 #pragma unroll
-            for (uint32_t b = 1; b < F; b++) {
-                const uint64_t zb = zc.z[P * F + b];
-                const uint32_t z0 = (uint32_t)zb, z1 = (uint32_t)(zb >> 32);
-#pragma unroll
-                for (uint32_t i = 0; i < OUTS; i += 4) {
-                    uint32_t p0[4], p1[4], s0[4], s1[4];
-                    glasm::mul_sb_x4((uint32_t)x[F * i + b], (uint32_t)(x[F * i + b] >> 32), z0, z1, p0[0], p1[0],
-                                     (uint32_t)x[F * (i + 1) + b], (uint32_t)(x[F * (i + 1) + b] >> 32), z0, z1, p0[1],
-                                     p1[1], (uint32_t)x[F * (i + 2) + b], (uint32_t)(x[F * (i + 2) + b] >> 32), z0, z1,
-                                     p0[2], p1[2], (uint32_t)x[F * (i + 3) + b], (uint32_t)(x[F * (i + 3) + b] >> 32),
-                                     z0, z1, p0[3], p1[3]);
-                    glasm::add_x4((uint32_t)h[i], (uint32_t)(h[i] >> 32), p0[0], p1[0], s0[0], s1[0],
-                                  (uint32_t)h[i + 1], (uint32_t)(h[i + 1] >> 32), p0[1], p1[1], s0[1], s1[1],
-                                  (uint32_t)h[i + 2], (uint32_t)(h[i + 2] >> 32), p0[2], p1[2], s0[2], s1[2],
-                                  (uint32_t)h[i + 3], (uint32_t)(h[i + 3] >> 32), p0[3], p1[3], s0[3], s1[3]);
-#pragma unroll
-                    for (int j = 0; j < 4; j++) h[i + j] = join2(s0[j], s1[j]);
-                }
-            }
+            for (uint32_t b = 1; b < F; b++) fold_term<OUTS, F>(h, x, b, zc.z[P * F + b], false);
 #pragma unroll
             for (uint32_t i = 0; i < OUTS; i += 4) canon4(h + i);
             store_fold_target<OUTS>(h, lds, P, t, dst, dst_col_stride, dst_shard_stride, c, q);
@@ -789,9 +832,9 @@ hipError_t launch_lde3_inv_fold(uint64_t* dst, size_t dst_col_stride, size_t dst
             acc = gl::mul(acc, s_pow_m[P]);
         }
     }
-    // F = 2 with targets in pairs (2P', 2P' + 1) whose s^m are negatives of each other (the
-    // collective's targets are: their shifts are s and s w_n): the butterfly form
-    uint32_t paired = log_f == 1 && shards % 2 == 0 && !getenv("BJ_INV_FOLD_UNPAIRED");
+    // targets in pairs (2P', 2P' + 1) whose s^m are negatives of each other (the collective's
+    // targets are, tests/test_fold_pairing.py): the even/odd form (at F = 2 the butterfly)
+    uint32_t paired = shards % 2 == 0 && !getenv("BJ_INV_FOLD_UNPAIRED");
     for (uint32_t P = 0; paired && P < shards; P += 2)
         paired = gl::canon(s_pow_m[P + 1]) == gl::canon(gl::sub(0, s_pow_m[P]));
 #define BJ_INVR(RR) \

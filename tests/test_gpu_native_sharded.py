@@ -451,11 +451,13 @@ def test_local_exchange_layouts():
             assert torch.equal(a2a[p * m:(p + 1) * m], i + 10**6 * p + 10**3 * P)
 
 
-@pytest.mark.parametrize("defer", [1, 99])
-def test_native_sharded_commit_leaves_deferred(torch_mod, defer):
-    """BJ_LEAVES_DEFER (collective.hip leaves_defer(), read once per process): chunk k's leaves
-    after chunk k + d's LDE, or after every LDE, must give the same commitment.  Run in a child
-    process, since the knob is read once."""
+@pytest.mark.parametrize("var,value", [("BJ_LEAVES_DEFER", "1"), ("BJ_LEAVES_DEFER", "99"),
+                                       ("BJ_INV_FOLD_UNPAIRED", "1")])
+def test_native_sharded_commit_env_knobs(torch_mod, var, value):
+    """The pipeline's experiment knobs must give the same commitment: BJ_LEAVES_DEFER
+    (collective.hip leaves_defer(), read once per process: chunk k's leaves after chunk k + d's
+    LDE, or after every LDE) and BJ_INV_FOLD_UNPAIRED (ntt_lde3.hip: the sender fold's
+    per-target loop instead of the paired even/odd form, F = 2, 4, 8).  Run in a child process."""
     import os
     import subprocess
     import sys
@@ -468,13 +470,15 @@ def test_native_sharded_commit_leaves_deferred(torch_mod, defer):
         "import torch, boojum_amd; boojum_amd.load()",
         "import test_gpu_native_sharded as T",
         "for world, cfg in [(8, (256, 13, 2, 16, 'poseidon2')), (2, (16, 18, 2, 16, 'poseidon2')),",
-        "                   (4, (16, 13, 1, 16, 'poseidon2')), (2, (16, 13, 2, 16, 'blake2s'))]:",
+        "                   (4, (16, 13, 1, 16, 'poseidon2')), (2, (16, 13, 2, 16, 'blake2s')),",
+        "                   (8, (16, 18, 2, 16, 'poseidon2')), (8, (16, 18, 1, 16, 'poseidon2')),",
+        "                   (8, (16, 18, 1, 16, 'poseidon2', 0)), (8, (16, 18, 2, 16, 'poseidon2', 1))]:",
         "    outs = T.run_local(torch, world, *cfg)",
         "    ref = T.reference(*cfg)",
         "    for P in range(world):",
         "        T.check_rank(ref, P, world, cfg[3], *outs[P], hasher=cfg[4])",
-        "print('deferred leaves ok')",
+        "print('knob ok')",
     ])
-    env = dict(os.environ, BJ_LEAVES_DEFER=str(defer))
-    r = subprocess.run([sys.executable, "-c", code], env=env, capture_output=True, text=True, timeout=240)
-    assert r.returncode == 0 and "deferred leaves ok" in r.stdout, r.stdout[-2000:] + r.stderr[-4000:]
+    env = dict(os.environ, **{var: value})
+    r = subprocess.run([sys.executable, "-c", code], env=env, capture_output=True, text=True, timeout=280)
+    assert r.returncode == 0 and "knob ok" in r.stdout, r.stdout[-2000:] + r.stderr[-4000:]

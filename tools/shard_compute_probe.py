@@ -14,7 +14,9 @@ import os
 import sys
 
 # PROBE_INTERFERE=1: also the same calls beside an exchange-shaped disturbance (interference());
-# PROBE_PHASE_EVENTS_TIMED=1 times those calls with the phase events on, as rounds 4-5 did
+# PROBE_PHASE_EVENTS_TIMED=1 times those calls with the phase events on, as rounds 4-5 did;
+# PROBE_LOG_K=k commits the first 2^k of the 2^log_lde cosets (k < D: at G > 2^k the sender folds
+# by F = G / 2^k)
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, os.path.join(ROOT, "era-boojum_amd"))
@@ -119,26 +121,27 @@ def main():
     out = {}
     for cfg, world in plan:
         n_cols, log_n, log_lde, cap = bench.CONFIGS[cfg]
+        log_k = int(os.environ.get("PROBE_LOG_K", log_lde))
         n = 1 << log_n
         comm = NativeComm.null(world, 0) if world > 1 else NativeComm.rccl_world1()
         tr = torch.empty((n_cols // world, n), dtype=torch.int64, device="cuda")
         for j, c in enumerate(native_columns(n_cols, world, 0)):
             call("bj_fill_synthetic_d", tr[j].data_ptr(), 1, n, log_n, 42, c, stream_of(tr))
-        res = NativeShardedResult(n_cols, log_n, log_lde, cap, world)
-        native_sharded_commit(comm, tr, n_cols, log_n, log_lde, cap, out=res)   # warm-up
+        res = NativeShardedResult(n_cols, log_n, log_lde, cap, world, log_commit_cosets=log_k)
+        native_sharded_commit(comm, tr, n_cols, log_n, log_lde, cap, out=res, log_commit_cosets=log_k)  # warm-up
         torch.cuda.synchronize()
         s, e = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
         reps = 3
         s.record()
         for _ in range(reps):
-            native_sharded_commit(comm, tr, n_cols, log_n, log_lde, cap, out=res)
+            native_sharded_commit(comm, tr, n_cols, log_n, log_lde, cap, out=res, log_commit_cosets=log_k)
         e.record()
         torch.cuda.synchronize()
         ms = s.elapsed_time(e) / reps
         # the same calls once more with the phase events on (bj_comm_set_timing)
         comm.set_timing(True)
         for _ in range(reps):
-            native_sharded_commit(comm, tr, n_cols, log_n, log_lde, cap, out=res)
+            native_sharded_commit(comm, tr, n_cols, log_n, log_lde, cap, out=res, log_commit_cosets=log_k)
         torch.cuda.synchronize()
         ph, calls = comm.phase_ms()
         comm.set_timing(False)
