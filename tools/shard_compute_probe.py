@@ -32,14 +32,14 @@ def links(world):
     return min(world - 1, 7)
 
 
-def _timed(comm, tr, res, n_cols, log_n, log_lde, cap, reps, phase_events_in_timed=False):
+def _timed(comm, tr, res, n_cols, log_n, log_lde, cap, reps, phase_events_in_timed=False, log_k=None):
     """ms per call (events around it on the compute stream) and the phase split.  The timed calls
     run as a production call does, without the library's phase events (bj_comm_set_timing), and
     the phase split comes from `reps` further calls with them on; phase_events_in_timed=True
     times the calls that record the phases (round 4 and round 5's r5o tables were taken so)."""
     import torch
     from boojum_amd.sharded import native_sharded_commit
-    native_sharded_commit(comm, tr, n_cols, log_n, log_lde, cap, out=res)  # warm-up
+    native_sharded_commit(comm, tr, n_cols, log_n, log_lde, cap, out=res, log_commit_cosets=log_k)  # warm-up
     torch.cuda.synchronize()
     comm.phase_ms()
 
@@ -49,7 +49,7 @@ def _timed(comm, tr, res, n_cols, log_n, log_lde, cap, reps, phase_events_in_tim
         for _ in range(reps):
             s, e = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
             s.record()
-            native_sharded_commit(comm, tr, n_cols, log_n, log_lde, cap, out=res)
+            native_sharded_commit(comm, tr, n_cols, log_n, log_lde, cap, out=res, log_commit_cosets=log_k)
             e.record()
             torch.cuda.synchronize()
             tot += s.elapsed_time(e)
@@ -62,7 +62,7 @@ def _timed(comm, tr, res, n_cols, log_n, log_lde, cap, reps, phase_events_in_tim
     return (ms_ev if ms is None else ms), {k: v / max(1, calls) for k, v in ph.items()}
 
 
-def interference(comm0, tr, res, n_cols, log_n, log_lde, cap, world, recv, reps, ph0, calls0):
+def interference(comm0, tr, res, n_cols, log_n, log_lde, cap, world, recv, reps, ph0, calls0, log_k=None):
     """The same call with each exchange replaced by an RCCL-shaped stand-in: a device-mode callback
     transport (bj_comm_init_callback) whose exchange launches tools/paced_copy.hip on the stream
     the library hands it -- the communicator's high-priority exchange stream, where RCCL's kernels
@@ -84,7 +84,7 @@ def interference(comm0, tr, res, n_cols, log_n, log_lde, cap, world, recv, reps,
     a_buf = torch.empty(ring // 8, dtype=torch.int64, device="cuda")
     b_buf = torch.empty_like(a_buf)
     ev = bool(os.environ.get("PROBE_PHASE_EVENTS_TIMED"))
-    base_ms, base_ph = _timed(comm0, tr, res, n_cols, log_n, log_lde, cap, reps, ev)
+    base_ms, base_ph = _timed(comm0, tr, res, n_cols, log_n, log_lde, cap, reps, ev, log_k)
     rows = {"phase_events_in_timed_calls": ev,
             "stubbed": {"ms": round(base_ms, 2), "phase_ms": {k: round(v, 2) for k, v in base_ph.items()}}}
     shapes = [("burst_32ch", 32, 0.0)]
@@ -98,7 +98,7 @@ def interference(comm0, tr, res, n_cols, log_n, log_lde, cap, world, recv, reps,
         fn = EXCHANGE_FN(exchange)
         comm = NativeComm._make("bj_comm_init_callback", world, 0, fn, None, 0, world=world, rank=0, keep=fn)
         try:
-            ms, ph = _timed(comm, tr, res, n_cols, log_n, log_lde, cap, reps, ev)
+            ms, ph = _timed(comm, tr, res, n_cols, log_n, log_lde, cap, reps, ev, log_k)
         finally:
             comm.close()
         rows[name] = {"ms": round(ms, 2), "delta_ms": round(ms - base_ms, 2),
@@ -150,7 +150,7 @@ def main():
             else 8 * n * n_cols * (world - 1) // world)
         interfered = None
         if recv and os.environ.get("PROBE_INTERFERE"):
-            interfered = interference(comm, tr, res, n_cols, log_n, log_lde, cap, world, recv, reps, ph, calls)
+            interfered = interference(comm, tr, res, n_cols, log_n, log_lde, cap, world, recv, reps, ph, calls, log_k)
         out["%s_G%d" % (cfg, world)] = {
             "interference": interfered,
             "ms_per_rank": round(ms, 2), "ideal_elems_per_s": n_cols * n / (ms * 1e-3),
