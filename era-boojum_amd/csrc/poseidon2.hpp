@@ -72,7 +72,8 @@ constexpr int SH[12] = {4, 14, 11, 8, 0, 5, 2, 9, 13, 6, 3, 12};
 // A 64-bit constant added into L: L < 2^39 after an external MDS, so L + c < 2^64 - 2^40
 // whenever c < 2^64 - 2^41.
 constexpr uint64_t FULL_RC_BOUND = ~0ull - (1ull << 41) + 1;
-// After the last partial round L, H < 2^61 (mi_layer_b_limbs), so W = Hhi EPS + L + c < 2^64
+// After the last partial round L < 2^60.1 and H < 2^61.1 (mi_layer_b_limbs on mi_layer_a_g's limbs,
+// tests/test_poseidon2_sched.py::test_partial_pair_limb_bounds), so W = Hhi EPS + L + c < 2^64
 // whenever c < 2^64 - 2^62; larger entries of rc26 go in as 32-bit limbs.
 constexpr uint64_t LIMB_RC_BOUND = (1ull << 63) + (1ull << 62);
 struct Values {
@@ -257,40 +258,57 @@ __device__ __forceinline__ void full_round(State& s, uint64_t* L, uint64_t* H, i
     mds_ext_limbs<OUT>(s.hi, H);
 }
 
-// Two partial rounds (pair q: rounds 4 + 2q, 5 + 2q) on the state as 64-bit register pairs Z
-// (the reductions' own output pairs, so the loop carries no 32-bit copies); Z[0] already holds
-// its round constant.  M_I of the first round leaves elements 1..11 as unreduced limbs
-// (< 2^46.6); only s0, the next S-box input, is reduced.  The second M_I consumes the limbs
-// (sums < 2^50.2, shifted terms < 2^61) and reduces every element.  Same field values as two
-// reduced rounds plus the schedule's offsets (glasm::mi_layer_a / mi_layer_b,
-// tools/gen_gl_asm.py).  The constants are read before the asm blocks (which the compiler does
-// not move loads across), so their scalar loads land during the first S-box.
-__device__ __forceinline__ void partial_round_pair(uint64_t* Z, int q) {
-    uint64_t L[12], H[12], z0;
+// Two partial rounds (pair q: rounds 4 + 2q, 5 + 2q).  The state enters as element 0 reduced
+// (z0, a 64-bit register pair already holding its round constant) and elements 1..11 either
+// reduced (W[i]; pair 0, after the full rounds) or half-reduced (HALF: W[i] + G[i] 2^32, as the
+// previous pair's mi_layer_b_half + eps_fold_x11 left them).  M_I of the first round leaves
+// elements 1..11 as unreduced limbs (< 2^47); only s0, the next S-box input, is reduced.  The
+// second M_I consumes the limbs (sums < 2^48, shifted terms < 2^61.1), reduces element 0 and
+// hands elements 1..11 on half-reduced: W = Hhi EPS + L (one mad) and G = Hlo, where the full
+// reduction took four instructions; the next first M_I takes G as a third limb (two mads more
+// per element), so a pair costs 11 instructions fewer (glasm::mi_layer_a_g / mi_layer_b_half,
+// tools/gen_gl_asm.py).  Same field values as two reduced rounds plus the schedule's offsets.
+// The constants are read before the asm blocks (which the compiler does not move loads across),
+// so their scalar loads land during the first S-box.
+struct Partial {
+    uint64_t z0;
+    uint64_t W[12];  // 1..11
+    uint32_t G[12];  // 1..11 (HALF)
+};
+
+template <bool HALF>
+__device__ __forceinline__ void partial_first(const Partial& P, int q, uint64_t* L, uint64_t* H, uint32_t& lo0,
+                                              uint32_t& hi0) {
+    uint64_t z0;
     uint32_t lo[12], hi[12];
-    const uint64_t kl = SCH.k_lo[q], kh = SCH.k_hi[q], dl = SCH.d_lo[q], dh = SCH.d_hi[q];
+    const uint64_t kl = SCH.k_lo[q], kh = SCH.k_hi[q];
+    split(P.z0, lo[0], hi[0]);
 #pragma unroll
-    for (int i = 0; i < 12; i++) split(Z[i], lo[i], hi[i]);
+    for (int i = 1; i < 12; i++) split(P.W[i], lo[i], hi[i]);
     sbox_x1(lo[0], hi[0]);
-    glasm::mi_layer_a(lo, hi, kl, kh, L, H, z0);
-    uint32_t lo0, hi0;
+    if constexpr (HALF) glasm::mi_layer_a_g(lo, hi, P.G, kl, kh, L, H, z0);
+    else glasm::mi_layer_a(lo, hi, kl, kh, L, H, z0);
     split(z0, lo0, hi0);
     sbox_x1(lo0, hi0);
-    glasm::mi_layer_b(lo0, hi0, L, H, dl, dh, Z);
+}
+
+template <bool HALF>
+__device__ __forceinline__ void partial_round_pair(Partial& P, int q) {
+    uint64_t L[12], H[12], Lo[12], Ho[12];
+    uint32_t lo0, hi0, hh[12];
+    const uint64_t dl = SCH.d_lo[q], dh = SCH.d_hi[q];
+    partial_first<HALF>(P, q, L, H, lo0, hi0);
+    glasm::mi_layer_b_half(lo0, hi0, L, H, dl, dh, Lo, Ho, P.z0);
+#pragma unroll
+    for (int i = 1; i < 12; i++) split(Ho[i], P.G[i], hh[i]);
+    glasm::eps_fold_x11(hh, Lo, P.W);
 }
 
 // The last pair (rounds 24, 25): the second M_I hands its limbs to the first full round.
-__device__ __forceinline__ void partial_round_pair_last(const uint64_t* Z, uint64_t* Lo, uint64_t* Ho) {
-    uint64_t L[12], H[12], z0;
-    uint32_t lo[12], hi[12];
-    const uint64_t kl = SCH.k_lo[10], kh = SCH.k_hi[10];
-#pragma unroll
-    for (int i = 0; i < 12; i++) split(Z[i], lo[i], hi[i]);
-    sbox_x1(lo[0], hi[0]);
-    glasm::mi_layer_a(lo, hi, kl, kh, L, H, z0);
+__device__ __forceinline__ void partial_round_pair_last(const Partial& P, uint64_t* Lo, uint64_t* Ho) {
+    uint64_t L[12], H[12];
     uint32_t lo0, hi0;
-    split(z0, lo0, hi0);
-    sbox_x1(lo0, hi0);
+    partial_first<true>(P, 10, L, H, lo0, hi0);
     glasm::mi_layer_b_limbs(lo0, hi0, L, H, Lo, Ho);
 }
 
@@ -314,6 +332,7 @@ __device__ __forceinline__ void add_rc26(uint64_t* L, uint64_t* H) {
 template <int OUT = OUT_ALL>
 __device__ __forceinline__ void permute(State& s) {
     uint64_t L[12], H[12], Z[12];
+    Partial P;
     mds_ext_limbs(s.lo, L);
     mds_ext_limbs(s.hi, H);
 #pragma unroll 1
@@ -327,9 +346,13 @@ __device__ __forceinline__ void permute(State& s) {
                          L[i + 2], (uint32_t)H[i + 2], (uint32_t)(H[i + 2] >> 32), Z[i + 2],
                          L[i + 3], (uint32_t)H[i + 3], (uint32_t)(H[i + 3] >> 32), Z[i + 3]);
     }
+    P.z0 = Z[0];
+#pragma unroll
+    for (int i = 1; i < 12; i++) P.W[i] = Z[i];
+    partial_round_pair<false>(P, 0);
 #pragma unroll 1
-    for (int q = 0; q < 10; q++) partial_round_pair(Z, q);
-    partial_round_pair_last(Z, L, H);
+    for (int q = 1; q < 10; q++) partial_round_pair<true>(P, q);
+    partial_round_pair_last(P, L, H);
     add_rc26(L, H);
     full_round<OUT_ALL, false>(s, L, H, 26);
 #pragma unroll 1

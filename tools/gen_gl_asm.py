@@ -312,7 +312,7 @@ LAYER_A_CHAINS = 1
 LAYER_B_CHAINS = 1
 
 
-def emit_mi_layer_a():
+def emit_mi_layer_a(with_g=False):
     """First partial round of a pair: M_I with elements 1..11 left as unreduced limbs.
     L_i = lo_i 2^SH[i] + sum lo_j + K_lo, H_i likewise (one mad each, < 2^46.6); only element
     0, the next S-box input, is reduced (into the 64-bit z0).  The pair's second round
@@ -320,7 +320,14 @@ def emit_mi_layer_a():
     values) starts the first sum chain in place of 0, so it costs nothing: it adds the field
     constant K_lo + K_hi 2^32 to every output.  poseidon2.hpp chooses K so that element 0 gets
     the next partial round's constant and carries the offset the other elements pick up
-    (p2::Sched)."""
+    (p2::Sched).
+
+    with_g (mi_layer_a_g, round 6): elements 1..11 arrive half-reduced from the previous pair's
+    mi_layer_b_half, as value = lo + hi 2^32 + G 2^32 with a third 32-bit limb G of the same
+    weight as hi.  G joins the H sum (11 more mads) and each H_i (one more mad: H_i =
+    G_i 2^SH[i] + (hi_i 2^SH[i] + Hs)), 22 instructions against the 33 the producer no longer
+    spends finishing its reductions.  Bounds: Ls < 13 * 2^32, Hs < 24 * 2^32, L_i < 2^46.0,
+    H_i < 2^47.0 (tests/test_poseidon2_sched.py::test_partial_pair_limb_bounds)."""
     pro = []
     consts, sreg = _consts(pro)
     NC = LAYER_A_CHAINS
@@ -336,6 +343,8 @@ def emit_mi_layer_a():
                 start = ("%%[K%s]" % limb) if c == 0 else "0"
                 ch.append(("v_mad_u64_u32 %s, %s, %%[%s%d], 1, %s" % (acc, JUNK, src, i, start if t == 0 else acc),
                            set(), {JUNK}))
+                if with_g and limb == "H" and i > 0:
+                    ch.append(("v_mad_u64_u32 %s, %s, %%[g%d], 1, %s" % (acc, JUNK, i, acc), set(), {JUNK}))
             chains.append(ch)
     body = pro + merge(chains)
     for limb in ("L", "H"):
@@ -347,19 +356,28 @@ def emit_mi_layer_a():
         K = consts.get(SH[i], str(1 << SH[i]))
         body.append(("v_mad_u64_u32 %%[L%d], %s, %%[lo%d], %s, %s" % (i, JUNK, i, K, Ls), set(), {JUNK}))
         body.append(("v_mad_u64_u32 %%[H%d], %s, %%[hi%d], %s, %s" % (i, JUNK, i, K, Hs), set(), {JUNK}))
+    if with_g:
+        for i in range(1, 12):
+            K = consts.get(SH[i], str(1 << SH[i]))
+            body.append(("v_mad_u64_u32 %%[H%d], %s, %%[g%d], %s, %%[H%d]" % (i, JUNK, i, K, i), set(), {JUNK}))
     body.append(("v_mad_u64_u32 v[12:13], %s, %%[lo0], %d, %s" % (JUNK, 1 << SH[0], Ls), set(), {JUNK}))
     body.append(("v_mad_u64_u32 v[14:15], %s, %%[hi0], %d, %s" % (JUNK, 1 << SH[0], Hs), set(), {JUNK}))
     body += reduce_limbs("v[12:13]", "v[14:15]", "v[16:17]", "v18", sp(0), "%[z0]")
     text = pad(body)
-    args = "const uint32_t* lo, const uint32_t* hi, uint64_t KL, uint64_t KH, uint64_t* L, uint64_t* H, uint64_t& z0"
+    name = "mi_layer_a_g" if with_g else "mi_layer_a"
+    args = "const uint32_t* lo, const uint32_t* hi, %suint64_t KL, uint64_t KH, uint64_t* L, uint64_t* H, uint64_t& z0" % (
+        "const uint32_t* g, " if with_g else "")
     outs = ['[z0] "=&v"(z0)']
     outs += ['[L%d] "=&v"(L[%d]), [H%d] "=&v"(H[%d])' % (i, i, i, i) for i in range(1, 12)]
     ins = ['[lo%d] "v"(lo[%d]), [hi%d] "v"(hi[%d])' % (i, i, i, i) for i in range(12)]
+    if with_g:
+        ins += ['[g%d] "v"(g[%d])' % (i, i) for i in range(1, 12)]
     ins += ['[KL] "s"(KL)', '[KH] "s"(KH)']
     clob = ['"v%d"' % i for i in range(20)] + ['"s%d"' % i for i in range(SGPR_BASE, sreg)]
     n_v = sum(1 for t in text if t.startswith("v_"))
-    lines = ["// Poseidon2 partial round M_I + K, first of a pair: elements 1..11 as limbs L, H (%d VALU instructions)" % n_v,
-             "__device__ __forceinline__ void mi_layer_a(%s) {" % args, "    asm volatile("]
+    what = ("elements 1..11 half-reduced in, " if with_g else "") + "elements 1..11 as limbs L, H"
+    lines = ["// Poseidon2 partial round M_I + K, first of a pair: %s (%d VALU instructions)" % (what, n_v),
+             "__device__ __forceinline__ void %s(%s) {" % (name, args), "    asm volatile("]
     lines += ['        "%s\\n"' % t for t in text]
     lines += ["        : %s" % ", ".join(outs), "        : %s" % ", ".join(ins), "        : %s);" % ", ".join(clob), "}"]
     return "\n".join(lines) + "\n"
@@ -479,6 +497,63 @@ def emit_mi_layer_b_limbs():
     return "\n".join(lines) + "\n"
 
 
+def emit_mi_layer_b_half():
+    """Second partial round of a pair, half-reduced hand-off (round 6): element 0 as in mi_layer_b
+    (+ D, reduced into the 64-bit z0: the next pair's S-box input), elements 1..11 left as the
+    limbs L_i', H_i' (< 2^60.1, < 2^61.1) of mi_layer_b_limbs.  eps_fold_x11 then forms
+    W_i = Hhi_i EPS + L_i' (< 2^62), and the next pair's mi_layer_a_g reads element i as
+    W_i + Hlo_i 2^32: one mad per element where the full reduction took four (the carry of
+    Hlo into W's high word, its EPS correction and the final mad are gone).  Hlo_i and Hhi_i are
+    the halves of the 64-bit output Ho[i]; the consumers take them as 32-bit operands, which the
+    compiler maps to the pair's sub-registers (inline asm cannot name a sub-register of its own
+    64-bit operand, hence the two blocks)."""
+    pro = []
+    consts, sreg = _consts(pro)
+    body = list(pro)
+    Ls, Hs = _layer_b_sums(body)
+    for g in range(3):
+        streams = []
+        for j in range(4):
+            i = 4 * g + j
+            if i == 0:
+                st = _layer_b_term(0, "v[8:9]", "v[10:11]", Ls, Hs, corr=True)
+                st += reduce_limbs("v[8:9]", "v[10:11]", "v[12:13]", "v14", sp(0), "%[z0]")
+            else:
+                st = _layer_b_term(i, "%%[Lo%d]" % i, "%%[Ho%d]" % i, Ls, Hs)
+            streams.append(st)
+        body += merge(streams)
+    text = pad(body)
+    args = ("uint32_t lo0, uint32_t hi0, const uint64_t* L, const uint64_t* H, uint64_t DL, uint64_t DH, "
+            "uint64_t* Lo, uint64_t* Ho, uint64_t& z0")
+    outs = ['[z0] "=&v"(z0)']
+    outs += ['[Lo%d] "=&v"(Lo[%d]), [Ho%d] "=&v"(Ho[%d])' % (i, i, i, i) for i in range(1, 12)]
+    ins = ['[lo0] "v"(lo0)', '[hi0] "v"(hi0)']
+    ins += ['[L%d] "v"(L[%d]), [H%d] "v"(H[%d])' % (i, i, i, i) for i in range(1, 12)]
+    ins += ['[DL] "s"(DL)', '[DH] "s"(DH)']
+    clob = ['"v%d"' % i for i in range(15)] + ['"s%d"' % i for i in range(SGPR_BASE, sreg)]
+    n_v = sum(1 for t in text if t.startswith("v_"))
+    lines = ["// Poseidon2 partial round M_I + D e_0, second of a pair: element 0 reduced, 1..11 as limbs (%d VALU instructions)" % n_v,
+             "__device__ __forceinline__ void mi_layer_b_half(%s) {" % args, "    asm volatile("]
+    lines += ['        "%s\\n"' % t for t in text]
+    lines += ["        : %s" % ", ".join(outs), "        : %s" % ", ".join(ins), "        : %s);" % ", ".join(clob), "}"]
+    return "\n".join(lines) + "\n"
+
+
+def emit_eps_fold():
+    """W_i = Hhi_i EPS + L_i for i = 1..11: the first step of the limb reduction, as mi_layer_b_half's
+    hand-off (Hhi_i the high half of its 64-bit H_i', passed as a 32-bit operand)."""
+    body = [("v_mad_u64_u32 %%[W%d], %s, %%[hh%d], -1, %%[L%d]" % (i, JUNK, i, i), set(), {JUNK}) for i in range(1, 12)]
+    text = pad(body)
+    args = "const uint32_t* hh, const uint64_t* L, uint64_t* W"
+    outs = ['[W%d] "=&v"(W[%d])' % (i, i) for i in range(1, 12)]
+    ins = ['[hh%d] "v"(hh[%d]), [L%d] "v"(L[%d])' % (i, i, i, i) for i in range(1, 12)]
+    lines = ["// W_i = Hhi_i * EPS + L_i, i = 1..11 (11 VALU instructions)",
+             "__device__ __forceinline__ void eps_fold_x11(%s) {" % args, "    asm volatile("]
+    lines += ['        "%s\\n"' % t for t in text]
+    lines += ["        : %s" % ", ".join(outs), "        : %s" % ", ".join(ins), "        : \"s%d\", \"s%d\");" % (SGPR_BASE + 24, SGPR_BASE + 25), "}"]
+    return "\n".join(lines) + "\n"
+
+
 SGPR_OPERANDS = True  # carry / constant SGPRs as compiler-allocated operands (False: fixed s40..)
 
 
@@ -570,6 +645,9 @@ namespace glasm {
     parts.append(emit_mi_layer_a())
     parts.append(emit_mi_layer_b())
     parts.append(emit_mi_layer_b_limbs())
+    parts.append(emit_mi_layer_a(with_g=True))
+    parts.append(emit_mi_layer_b_half())
+    parts.append(emit_eps_fold())
     parts.append("}  // namespace glasm\n")
     parts = [sgpr_operandize(x) for x in parts]
     with open(args.out, "w") as f:

@@ -2,14 +2,15 @@
 """Static VALU census of one Poseidon2 permutation as compiled for gfx950.
 
 The permutation (csrc/poseidon2.hpp) has three `#pragma unroll 1` round loops with fixed
-trip counts: 4 full rounds, 10 pairs of partial rounds and 2 full rounds (peeled: the last pair
+trip counts: 4 full rounds, 9 pairs of partial rounds (pair 0, which takes reduced words, is peeled;
+round 6) and 2 full rounds (peeled: the last pair
 of partial rounds, which hands limbs to the first full round after it; that round, which takes
 its constants from the schedule; and the last full round, so that its MDS forms only the outputs
 the caller reads). The census kernels of
 tools/census_perm.hip run exactly one permutation per lane in each output form (all 12
 words, the capacity words, the digest), so their dynamic instruction stream is known
 statically:
-    straight-line code x1 + loop bodies x (4, 10, 2).
+    straight-line code x1 + loop bodies x (4, 9, 2).
 This tool disassembles the gfx950 code object and weights each VALU instruction by the
 issue cost measured in profiles/r1_isa_rates.txt:
 * 1 slot: full-rate 32-bit ops (v_add_u32, v_mov_b32, logic);
@@ -76,7 +77,7 @@ def parse(lines):
     return instrs
 
 
-def census(instrs, trips=(4, 10, 2)):
+def census(instrs, trips=(4, 9, 2)):
     base = instrs[0][0]
     back = [(i, a, t) for i, (a, mn, t) in enumerate(instrs) if t is not None and base + t < a]
     if len(back) != len(trips):
