@@ -24,6 +24,7 @@ EXCHANGE_FN = ctypes.CFUNCTYPE(ctypes.c_int, ctypes.c_void_p, ctypes.c_int, ctyp
 SIGNATURES = {
     "bj_last_error": ([], ctypes.c_char_p),
     "bj_abi_version": ([], _u32),
+    "bj_experiment_knob": ([ctypes.c_char_p, _u64p], _int),
     "bj_release_workspace": ([], _int),
     "bj_release_tables": ([], _int),
     "bj_prepare": ([_u32], _int),

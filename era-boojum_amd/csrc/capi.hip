@@ -214,12 +214,10 @@ int get_lde3_lde(uint32_t log_n, uint32_t log_d, const uint64_t** out) {
                         }, out);
 }
 
-// The three-pass LDE (ntt_lde3.hip) is the default for 2^18..2^23; BJ_LDE_PASSES=2 selects the
-// two-pass CT path (head + tail per transform) instead, for same-binary A/B measurements.
-bool use_lde3(uint32_t log_n) {
-    const char* v = getenv("BJ_LDE_PASSES");
-    return !(v && v[0] == '2') && bj::lde3_supported(log_n);
-}
+// The three-pass LDE (ntt_lde3.hip) is the default for 2^18..2^23; BJ_LDE_PASSES=2 (an experiment
+// knob, bj_internal.hpp) selects the two-pass CT path (head + tail per transform) instead, for
+// same-binary A/B measurements.
+bool use_lde3(uint32_t log_n) { return bj::knobs().lde_passes != 2 && bj::lde3_supported(log_n); }
 
 inline bool is_pow2(size_t x) { return x && !(x & (x - 1)); }
 
@@ -467,7 +465,19 @@ hipError_t pool_alloc(void** p, size_t bytes, hipStream_t st) {
 extern "C" {
 
 const char* bj_last_error(void) { return g_err.c_str(); }
-uint32_t bj_abi_version(void) { return (2u << 16) | 5u; }
+uint32_t bj_abi_version(void) { return (2u << 16) | 6u; }
+
+int bj_experiment_knob(const char* name, uint64_t* value) {
+    if (!name || !value) return fail(BJ_EINVAL, "bj_experiment_knob: null argument");
+    const bj::Knobs& k = bj::knobs();
+    if (!strcmp(name, "BJ_EXPERIMENTS")) *value = k.enabled;
+    else if (!strcmp(name, "BJ_LEAVES_DEFER")) *value = k.leaves_defer;
+    else if (!strcmp(name, "BJ_INV_FOLD_UNPAIRED")) *value = k.inv_fold_unpaired;
+    else if (!strcmp(name, "BJ_LDE_PASSES")) *value = k.lde_passes;
+    else if (!strcmp(name, "BJ_NODE_Q4_MAX")) *value = k.node_q4_max;
+    else return fail(BJ_EINVAL, std::string("bj_experiment_knob: unknown knob ") + name);
+    return BJ_OK;
+}
 
 int bj_release_workspace(void) {
     HIP_TRY(bj::pool_trim_all(), "hipMemPoolTrimTo");

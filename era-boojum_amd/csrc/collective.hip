@@ -331,16 +331,10 @@ uint32_t log2u(uint64_t x) {
     return l;
 }
 
-// BJ_LEAVES_DEFER=d (experiments, tools/shard_compute_probe.py): chunk k's leaves are issued
+// BJ_LEAVES_DEFER=d (an experiment knob, bj_internal.hpp; tools/shard_compute_probe.py): chunk k's leaves are issued
 // after chunk k + d's LDE instead of right after its own (d = 0), so fewer LDE -> leaf switches
 // happen on the compute stream; larger d needs the later chunks' exchanges earlier.
-size_t leaves_defer() {
-    static const size_t v = [] {
-        const char* e = getenv("BJ_LEAVES_DEFER");
-        return e ? (size_t)strtoull(e, nullptr, 0) : (size_t)0;
-    }();
-    return v;
-}
+size_t leaves_defer() { return (size_t)bj::knobs().leaves_defer; }
 
 struct Run {
     uint32_t lo, global, count;  // local first row, global first column, columns

@@ -300,13 +300,7 @@ hipError_t launch_leaves_chunked(const uint64_t* src, size_t col_stride, uint32_
     return hipGetLastError();
 }
 
-static size_t node_q4_max() {
-    static const size_t v = [] {
-        const char* e = getenv("BJ_NODE_Q4_MAX");
-        return e ? (size_t)strtoull(e, nullptr, 0) : (size_t)1 << 15;
-    }();
-    return v;
-}
+static size_t node_q4_max() { return (size_t)knobs().node_q4_max; }
 
 hipError_t launch_nodes(const uint64_t* leaves, size_t n_leaves, uint32_t cap_size, uint64_t* nodes,
                         hipStream_t st) {

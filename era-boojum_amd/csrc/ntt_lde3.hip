@@ -834,7 +834,7 @@ hipError_t launch_lde3_inv_fold(uint64_t* dst, size_t dst_col_stride, size_t dst
     }
     // targets in pairs (2P', 2P' + 1) whose s^m are negatives of each other (the collective's
     // targets are, tests/test_fold_pairing.py): the even/odd form (at F = 2 the butterfly)
-    uint32_t paired = shards % 2 == 0 && !getenv("BJ_INV_FOLD_UNPAIRED");
+    uint32_t paired = shards % 2 == 0 && !knobs().inv_fold_unpaired;
     for (uint32_t P = 0; paired && P < shards; P += 2)
         paired = gl::canon(s_pow_m[P + 1]) == gl::canon(gl::sub(0, s_pow_m[P]));
 #define BJ_INVR(RR) \

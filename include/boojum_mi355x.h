@@ -49,6 +49,16 @@ const char* bj_last_error(void);
 /* ABI version (major << 16 | minor). */
 uint32_t bj_abi_version(void);
 
+/* The value in effect of one experiment knob (ABI 2.6; no reference counterpart).  The library's
+ * same-binary A/B switches -- BJ_LEAVES_DEFER (default 0), BJ_INV_FOLD_UNPAIRED (0),
+ * BJ_LDE_PASSES (3) and BJ_NODE_Q4_MAX (32768) -- are read from the environment only when
+ * BJ_EXPERIMENTS=1 is set, once per process at the first call that needs one; otherwise each
+ * keeps its production value, so a prover's environment cannot change the kernel schedule (the
+ * reference's transform_raw_storages_to_lde, cs/implementations/utils.rs:270-403, is a pure
+ * function of its inputs).  Every setting gives the same outputs.  name "BJ_EXPERIMENTS" reports
+ * the gate (0 / 1).  BJ_EINVAL for an unknown name.  Host-only: touches no device. */
+int bj_experiment_knob(const char* name, uint64_t* value);
+
 /* Fill the device twiddle cache for FFT size 2^log_n (forward + inverse tables) on the
  * current device, synchronously.  Twiddle precompute is outside the timed region in
  * the reference's own accounting (prover.rs:313-353 precomputes before "LDE taken").

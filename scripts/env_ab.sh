@@ -4,6 +4,8 @@
 set -u
 TAG=$1; VAR=$2; A=$3; B=$4; shift 4
 cd "$GRAFT_REPO_ROOT" && mkdir -p gpurun_out/$TAG && export TMPDIR=/tmp
+# the library reads its experiment knobs only under this gate (bj_internal.hpp, ABI 2.6)
+export BJ_EXPERIMENTS=1
 for i in 1 2 3; do
   for V in "$A" "$B"; do
     N=${V:-unset}

@@ -19,6 +19,10 @@ P = O.P
 
 @pytest.fixture(scope="module")
 def bj():
+    return make_bj()
+
+
+def make_bj():
     import torch
     assert torch.cuda.is_available(), "gpu tests need a GPU"
     import boojum_amd
@@ -75,14 +79,33 @@ def test_lde3_strided_trace(bj):
 
 @pytest.mark.parametrize("log_n,log_d", [(20, 1), (22, 2)])
 def test_lde3_equals_two_pass_path(bj, log_n, log_d):
-    """Same binary, BJ_LDE_PASSES=2 (head + tail per transform) against the default three passes."""
+    """Same binary, BJ_LDE_PASSES=2 (head + tail per transform) against the default three passes.
+    The library reads its experiment knobs once per process and only under BJ_EXPERIMENTS=1
+    (bj_internal.hpp), so the two-pass form runs in a child process and writes its LDE to a file."""
+    import subprocess
+    import sys
+    import tempfile
     x = rand((4, 1 << log_n), 4200 + log_n)
     a, ma = lde_d(bj, x, log_d)
-    os.environ["BJ_LDE_PASSES"] = "2"
-    try:
-        b, mb = lde_d(bj, x, log_d)
-    finally:
-        del os.environ["BJ_LDE_PASSES"]
+    here = os.path.dirname(os.path.abspath(__file__))
+    root = os.path.dirname(here)
+    with tempfile.TemporaryDirectory() as td:
+        np.save(os.path.join(td, "x.npy"), x)
+        code = "\n".join([
+            "import sys; sys.path[:0] = [%r, %r, %r, %r]" % (os.path.join(root, "oracle"),
+                                                            os.path.join(root, "era-boojum_amd"), root, here),
+            "import ctypes, numpy as np, test_gpu_lde3 as T",
+            "bj = T.make_bj()",
+            "from boojum_amd._lib import load",
+            "v = ctypes.c_uint64(0); assert load().bj_experiment_knob(b'BJ_LDE_PASSES', ctypes.byref(v)) == 0",
+            "assert v.value == 2, v.value",
+            "l, m = T.lde_d(bj, np.load(%r), %d)" % (os.path.join(td, "x.npy"), log_d),
+            "np.save(%r, l); np.save(%r, m)" % (os.path.join(td, "l.npy"), os.path.join(td, "m.npy")),
+            "print('two-pass ok')"])
+        env = dict(os.environ, BJ_EXPERIMENTS="1", BJ_LDE_PASSES="2")
+        r = subprocess.run([sys.executable, "-c", code], env=env, capture_output=True, text=True, timeout=200)
+        assert r.returncode == 0 and "two-pass ok" in r.stdout, r.stdout[-2000:] + r.stderr[-4000:]
+        b, mb = np.load(os.path.join(td, "l.npy")), np.load(os.path.join(td, "m.npy"))
     eq(a, b)
     eq(ma, mb)
 

@@ -468,7 +468,9 @@ def test_native_sharded_commit_env_knobs(torch_mod, var, value):
                                                         os.path.join(os.path.dirname(here), "era-boojum_amd"),
                                                         os.path.dirname(here), here),
         "import torch, boojum_amd; boojum_amd.load()",
-        "import test_gpu_native_sharded as T",
+        "import test_gpu_native_sharded as T, ctypes",
+        "v = ctypes.c_uint64(0); assert boojum_amd._lib.load().bj_experiment_knob(%r, ctypes.byref(v)) == 0" % var.encode(),
+        "assert v.value == int(%r), v.value" % value,
         "for world, cfg in [(8, (256, 13, 2, 16, 'poseidon2')), (2, (16, 18, 2, 16, 'poseidon2')),",
         "                   (4, (16, 13, 1, 16, 'poseidon2')), (2, (16, 13, 2, 16, 'blake2s')),",
         "                   (8, (16, 18, 2, 16, 'poseidon2')), (8, (16, 18, 1, 16, 'poseidon2')),",
@@ -479,6 +481,6 @@ def test_native_sharded_commit_env_knobs(torch_mod, var, value):
         "        T.check_rank(ref, P, world, cfg[3], *outs[P], hasher=cfg[4])",
         "print('knob ok')",
     ])
-    env = dict(os.environ, **{var: value})
+    env = dict(os.environ, BJ_EXPERIMENTS="1", **{var: value})
     r = subprocess.run([sys.executable, "-c", code], env=env, capture_output=True, text=True, timeout=280)
     assert r.returncode == 0 and "knob ok" in r.stdout, r.stdout[-2000:] + r.stderr[-4000:]

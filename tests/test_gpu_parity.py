@@ -335,13 +335,16 @@ def test_node_levels_one_per_lane(bj):
         "import numpy as np, oracle as O\n"
         "from boojum_amd import field, merkle\n"
         "src = np.random.default_rng(5).integers(0, O.P, size=(9, 1 << 15), dtype=np.uint64)\n"
+        "import ctypes; from boojum_amd._lib import load\n"
+        "v = ctypes.c_uint64(9); assert load().bj_experiment_knob(b'BJ_NODE_Q4_MAX', ctypes.byref(v)) == 0\n"
+        "assert v.value == 0, v.value\n"
         "for cap in (1, 16, 512):\n"
         "    tree = merkle.MerkleTreeWithCap.construct(field.to_device(src), cap)\n"
         "    leaves, nodes, levels, capr = O.merkle_construct(src, cap, threads=4)\n"
         "    assert np.array_equal(field.to_host(tree.nodes), nodes), cap\n"
         "    assert np.array_equal(tree.get_cap(), capr), cap\n"
         "print('lane-form tree ok')\n")
-    env = dict(os.environ, BJ_NODE_Q4_MAX="0")
+    env = dict(os.environ, BJ_EXPERIMENTS="1", BJ_NODE_Q4_MAX="0")
     root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
     env["PYTHONPATH"] = os.pathsep.join([os.path.join(root, "era-boojum_amd"), os.path.join(root, "oracle"),
                                          env.get("PYTHONPATH", "")])
@@ -514,7 +517,7 @@ def test_release_workspace_between_host_commits(bj):
     commit re-allocates its workspace and is still bit-exact."""
     import ctypes
     from boojum_amd._lib import call, load
-    assert load().bj_abi_version() == (2 << 16) | 5
+    assert load().bj_abi_version() == (2 << 16) | 6
     c, log_n, log_d, cap = 40, 14, 2, 16
     tr = O.synthetic_trace(c, log_n)
     ref = O.lde_commit(tr, log_d, cap, threads=8)
