@@ -88,9 +88,11 @@ class NativeComm:
         return out.as_dict()
 
     def check_world(self, stream=None):
-        """bj_comm_check_world (collective): every rank's info, gathered; raises BoojumError when
-        the transport's world is not this communicator's (count, rank order) or, for RCCL, when two
-        ranks drive one device.  Returns (ok, [info per rank], message)."""
+        """bj_comm_check_world (collective): every rank's info, gathered.  Returns (ok, [info per
+        rank], message): ok is False, with the library's message, when the transport's world is not
+        this communicator's (count, rank order), when two RCCL ranks drive one device, or when a
+        rank could not read its own record (BJ_EINVAL on every rank).  Only a transport or HIP
+        error raises BoojumError."""
         from ._lib import BoojumError, CommInfo
         out = (CommInfo * self.world)()
         rc = load().bj_comm_check_world(self.handle, out, stream)
@@ -171,6 +173,35 @@ class NativeComm:
         commitment (the received buffers are never filled)."""
         fn = _EXCHANGE_FN(lambda *a: 0)
         return cls._make("bj_comm_init_callback", world, rank, fn, None, 0, world=world, rank=rank, keep=fn)
+
+    def link_probe(self, kind, bytes_per_rank, stream=None):
+        """Time one bj_comm_exchange_d of `kind` (XCHG_ALL_GATHER / XCHG_ALL_TO_ALL) with
+        `bytes_per_rank` bytes per rank block, as bj_sharded_commit_d's exchanges move them
+        (collective; every rank calls it).  A small exchange of the same kind first sets up the
+        transport's connections; the caller should hold the ranks at a barrier just before.
+        Returns the milliseconds between HIP events on `stream` around the exchange: the
+        transport's time plus any wait for peers that reached it later (so the minimum over ranks
+        is the closest to the link's own time)."""
+        dev = torch.device("cuda", torch.cuda.current_device())
+        st = stream if stream is not None else torch.cuda.current_stream().cuda_stream
+        world = self.world
+        words = max(1, bytes_per_rank // 8)
+        nsend = words * (world if kind == XCHG_ALL_TO_ALL else 1)
+        send = torch.zeros(nsend, dtype=torch.int64, device=dev)
+        recv = torch.empty(words * world, dtype=torch.int64, device=dev)
+        check(load().bj_comm_exchange_d(self.handle, kind, send.data_ptr(), recv.data_ptr(), 8, st),
+              "bj_comm_exchange_d")
+        torch.cuda.synchronize()
+        s_ = torch.cuda.ExternalStream(st) if stream is not None else torch.cuda.current_stream()
+        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        e0.record(s_)
+        check(load().bj_comm_exchange_d(self.handle, kind, send.data_ptr(), recv.data_ptr(), words * 8, st),
+              "bj_comm_exchange_d")
+        e1.record(s_)
+        torch.cuda.synchronize()
+        ms = e0.elapsed_time(e1)
+        del send, recv
+        return ms
 
     def set_timing(self, on=True):
         """Record phase events in every later bj_sharded_commit_d call (bj_comm_set_timing)."""

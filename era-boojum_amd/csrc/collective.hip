@@ -620,23 +620,46 @@ int bj_comm_info(bj_comm* c, bj_comm_info_t* out) {
 int bj_comm_check_world(bj_comm* c, bj_comm_info_t* all_out, void* stream) {
     if (!c || !all_out) return err(BJ_EINVAL, "null argument");
     static_assert(sizeof(bj_comm_info_t) == 128, "bj_comm_info_t is 128 bytes");
+    // every rank enters the gather, also one whose own record failed: it sends a
+    // record marked invalid, so its peers fail with the same BJ_EINVAL instead of waiting in the
+    // collective for a rank that returned early
     bj_comm_info_t mine;
-    BJ_CHECK(bj_comm_info(c, &mine));
+    const int info_rc = bj_comm_info(c, &mine);
+    std::string info_err;
+    if (info_rc != BJ_OK) {
+        info_err = bj_last_error();
+        std::memset(&mine, 0, sizeof(mine));
+        mine.kind = BJ_COMM_INVALID;
+        mine.world = c->world;
+        mine.rank = c->rank;
+        mine.transport_count = c->world;
+        mine.transport_rank = c->rank;
+        mine.reserved[0] = info_rc;
+        if (gethostname(mine.host, sizeof(mine.host) - 1) != 0) mine.host[0] = 0;
+    }
     hipStream_t st = reinterpret_cast<hipStream_t>(stream);
     const size_t rec = sizeof(bj_comm_info_t);
     void* dev = nullptr;
+    // the one local failure that cannot enter the gather (no buffer to gather into)
     HIP_CHECK(hipMalloc(&dev, rec * (c->world + 1)), "hipMalloc");
     char* send = static_cast<char*>(dev) + rec * c->world;
-    int rc = BJ_OK;
+    // a failed copy still enters the gather: the peers then see a slot that does not match
     hipError_t e = hipMemcpyAsync(send, &mine, rec, hipMemcpyHostToDevice, st);
-    if (e == hipSuccess) {
-        rc = all_gather(c, send, dev, rec, st);
-        if (rc == BJ_OK) e = hipMemcpyAsync(all_out, dev, rec * c->world, hipMemcpyDeviceToHost, st);
-        if (rc == BJ_OK && e == hipSuccess) e = hipStreamSynchronize(st);
+    int rc = all_gather(c, send, dev, rec, st);
+    if (rc == BJ_OK) {
+        const hipError_t e2 = hipMemcpyAsync(all_out, dev, rec * c->world, hipMemcpyDeviceToHost, st);
+        const hipError_t e3 = hipStreamSynchronize(st);
+        if (e == hipSuccess) e = e2 != hipSuccess ? e2 : e3;
     }
     (void)hipFree(dev);
     if (rc) return rc;
     if (e != hipSuccess) return err(BJ_EHIP, std::string("bj_comm_check_world: ") + hipGetErrorString(e));
+    for (int p = 0; p < c->world; p++)
+        if (all_out[p].kind == BJ_COMM_INVALID)
+            return err(BJ_EINVAL, "bj_comm_check_world: rank " + std::to_string(all_out[p].rank) +
+                                      " could not read its transport record (code " +
+                                      std::to_string(all_out[p].reserved[0]) + ")" +
+                                      (info_err.empty() ? std::string() : ": " + info_err));
     // what the transport saw: every rank in its own slot, the transport's count and rank equal to
     // the communicator's; an RCCL world with one device per rank (the local and callback
     // transports may share a device by design: ranks as threads, a rehearsal over gloo)

@@ -369,6 +369,7 @@ int bj_comm_destroy(bj_comm* comm);
 #define BJ_COMM_RCCL 0
 #define BJ_COMM_LOCAL 1
 #define BJ_COMM_CALLBACK 2
+#define BJ_COMM_INVALID (-1) /* bj_comm_check_world: the rank could not read its record; reserved[0] = its error */
 typedef struct bj_comm_info_t {
     int32_t kind;
     int32_t world, rank;
@@ -384,7 +385,10 @@ int bj_comm_info(bj_comm* comm, bj_comm_info_t* out);
  * p, and every rank's transport count and rank equal the communicator's world and rank; for RCCL
  * also that no two ranks drive one device (same host and PCI bus id, or same device number where
  * the bus id is unknown).  BJ_EINVAL naming the ranks otherwise (all_out is filled either way once
- * the gather ran).  The local and callback transports may share a device by design. */
+ * the gather ran).  The local and callback transports may share a device by design.  A rank whose
+ * own bj_comm_info fails still enters the gather with a record of kind BJ_COMM_INVALID, so every
+ * rank returns BJ_EINVAL; only a failed device allocation (128 * (world + 1) bytes) returns before
+ * the gather, and then the peers wait in the transport's collective. */
 int bj_comm_check_world(bj_comm* comm, bj_comm_info_t* all_out, void* stream);
 /* One data exchange of bj_sharded_commit_d's kinds (BJ_XCHG_ALL_GATHER / BJ_XCHG_ALL_TO_ALL, the
  * layouts above) over `comm`, ordered on `stream`: the transport alone, so a caller can check its

@@ -226,7 +226,10 @@ typedef struct {
     const uint8_t* uid;     /* RCCL (bj_comm_init_rccl) over this unique id */
     int rank, world;
     uint32_t n_cols, log_n, log_lde, log_k, cap;
-    int check_world;        /* RCCL: 1 expect bj_comm_check_world to pass, -1 to reject a shared device */
+    int check_world;        /* RCCL: 1 expect bj_comm_check_world to pass (then time one exchange of the
+                             * run's kind and size, as bench.py's "link" does), -1 to reject a shared
+                             * device, 2 to reject a rank whose own record failed (the mock's
+                             * MOCK_RCCL_FAIL_INFO_RANK) on every rank */
     const u64* trace; /* all columns, host */
     u64* leaves;      /* all leaves, host: rank P writes its range */
     u64* cap_out;     /* this rank's gathered cap */
@@ -269,7 +272,18 @@ static void* rank_worker(void* p) {
     bj_comm* comm = NULL;
     j->rc = j->group ? bj_comm_init_local(j->group, j->rank, &comm) : bj_comm_init_rccl(j->uid, j->world, j->rank, &comm);
     if (j->rc) return NULL;
-    if (j->check_world) {
+    if (j->check_world == 2) {
+        /* one rank cannot read its transport record: it still enters the gather, so every rank
+         * returns BJ_EINVAL instead of its peers waiting for it */
+        bj_comm_info_t all[64];
+        int rc = bj_comm_check_world(comm, all, st);
+        if (rc != BJ_EINVAL || !strstr(bj_last_error(), "could not read its transport record")) {
+            fprintf(stderr, "rank %d: bj_comm_check_world rc %d (%s), expected an invalid-record rejection\n",
+                    j->rank, rc, bj_last_error());
+            j->rc = -1;
+            return NULL;
+        }
+    } else if (j->check_world) {
         /* what RCCL's API reports for this rank (ncclCommCount / UserRank / CuDevice), then the
          * collective world check: a shared device must be rejected, distinct ones accepted */
         bj_comm_info_t info, all[64];
@@ -296,6 +310,37 @@ static void* rank_worker(void* p) {
                 j->rc = -1;
                 return NULL;
             }
+        if (j->check_world > 0) {
+            /* the link probe bench.py runs before an N > 1 line's timed region (its "link"
+             * object): one bj_comm_exchange_d of the commit's kind and size -- G <= D the
+             * all-gather of 8 n C/G bytes per rank, G > D the all-to-all of 8 m C/G per
+             * destination and block -- after a small exchange that sets up the transport */
+            const int a2a = j->world > (1 << j->log_lde);
+            const size_t block = a2a ? 8 * m * cpr * blocks : 8 * n * cpr;
+            const int kind = a2a ? BJ_XCHG_ALL_TO_ALL : BJ_XCHG_ALL_GATHER;
+            void *snd, *rcv;
+            HIPC(hipMalloc(&snd, a2a ? block * j->world : block));
+            HIPC(hipMalloc(&rcv, block * j->world));
+            HIPC(hipMemsetAsync(snd, 0, a2a ? block * j->world : block, st));
+            hipEvent_t e0, e1;
+            HIPC(hipEventCreate(&e0));
+            HIPC(hipEventCreate(&e1));
+            j->rc = bj_comm_exchange_d(comm, kind, snd, rcv, 8, st);
+            if (j->rc == 0) {
+                HIPC(hipStreamSynchronize(st));
+                HIPC(hipEventRecord(e0, st));
+                j->rc = bj_comm_exchange_d(comm, kind, snd, rcv, block, st);
+                HIPC(hipEventRecord(e1, st));
+                HIPC(hipStreamSynchronize(st));
+            }
+            float ms = 0;
+            HIPC(hipEventElapsedTime(&ms, e0, e1));
+            hipEventDestroy(e0); hipEventDestroy(e1); hipFree(snd); hipFree(rcv);
+            if (j->rc) return NULL;
+            const size_t peer_bytes = (size_t)(j->world - 1) * block;
+            printf("link world %d rank %d kind %s bytes_per_rank %zu ms %.3f gbs_per_rank %.2f\n", j->world, j->rank,
+                   a2a ? "all_to_all" : "all_gather", peer_bytes, ms, ms > 0 ? peer_bytes / ms / 1e6 : 0.0);
+        }
     }
     j->rc = bj_sharded_commit_d(comm, tr, n, j->n_cols, j->log_n, j->log_lde, j->log_k, j->cap, BJ_HASHER_POSEIDON2,
                                 lde, leaves, nodes, cap, st);
@@ -440,6 +485,12 @@ int main(int argc, char** argv) {
                 check_sharded(log_n, n_cols, log_lde, log_k, cap, world, 1, -1);
                 setenv("MOCK_RCCL_FAKE_DEVICES", "1", 1);
                 check_sharded(log_n, n_cols, log_lde, log_k, cap, world, 1, 1);
+                /* a rank whose transport record fails: every rank gets BJ_EINVAL, none waits */
+                char fail_rank[16];
+                snprintf(fail_rank, sizeof(fail_rank), "%d", world - 1);
+                setenv("MOCK_RCCL_FAIL_INFO_RANK", fail_rank, 1);
+                check_sharded(log_n, n_cols, log_lde, log_k, cap, world, 1, 2);
+                unsetenv("MOCK_RCCL_FAIL_INFO_RANK");
                 unsetenv("MOCK_RCCL_FAKE_DEVICES");
                 worlds_checked |= world;
             }
@@ -451,7 +502,7 @@ int main(int argc, char** argv) {
     }
     if (mock)
         printf("rccl world check ok at world%s%s%s: ncclCommCount = world, ncclCommUserRank = rank, shared device "
-               "rejected, distinct devices accepted\n", worlds_checked & 2 ? " 2" : "", worlds_checked & 4 ? " 4" : "",
+               "rejected, distinct devices accepted, a failed record rejected on every rank; link probe at each\n", worlds_checked & 2 ? " 2" : "", worlds_checked & 4 ? " 4" : "",
                worlds_checked & 8 ? " 8" : "");
     printf("c_caller ok%s: 2^%u x %u, LDE x%u, %u cosets committed, cap %u, %d seam threads; "
            "cap[0] = %016llx %016llx %016llx %016llx\n",

@@ -248,6 +248,10 @@ ncclResult_t ncclCommUserRank(const ncclComm_t comm, int* rank) {
 
 ncclResult_t ncclCommCuDevice(const ncclComm_t comm, int* device) {
     if (!comm || !device) return ncclInvalidArgument;
+    // MOCK_RCCL_FAIL_INFO_RANK=r: rank r cannot report its device (bj_comm_check_world must still
+    // enter the gather, and every rank must get the same rejection)
+    const char* f = getenv("MOCK_RCCL_FAIL_INFO_RANK");
+    if (f && atoi(f) == comm->rank) return ncclInternalError;
     *device = comm->device;
     return ncclSuccess;
 }

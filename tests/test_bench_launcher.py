@@ -92,3 +92,27 @@ def test_world_record_from_gathered_infos():
     rec = bench.world_record(shared, "gloo", "ranks 0 and 1 share device 0")
     assert rec["backend"] == "gloo (callback transport)" and rec["distinct_devices"] == 1
     assert rec["check"] == "ranks 0 and 1 share device 0"
+
+
+def test_link_record_schema():
+    """The N > 1 line's "link" object (bench.link_record): one exchange of the run's own kind and
+    size, timed on every rank before the timed region; min / max over ranks.  The exchange shapes
+    are bj_sharded_commit_d's: C3 at G = 4 all-gathers 2 GiB per rank block (6 GiB
+    from peers), at G = 8 > D one all-to-all of 512 MiB per destination (3.5 GiB from peers)."""
+    import bench
+    assert bench.exchange_shape(256, 22, 2, 4) == ("all_gather", 2 << 30)
+    assert bench.exchange_shape(256, 22, 2, 8) == ("all_to_all", 512 << 20)
+    assert bench.exchange_shape(256, 23, 3, 8) == ("all_gather", 2 << 30)           # C4: G = D
+    assert bench.exchange_shape(128, 20, 1, 8) == ("all_to_all", 32 << 20)          # C2 at G = 8
+    assert bench.exchange_shape(16, 18, 3, 8, log_commit_cosets=1) == ("all_gather", 4 << 20)
+    assert bench.exchange_shape(16, 18, 2, 8, log_commit_cosets=1) == ("all_to_all", 8 * (1 << 16) * 2 * 2)
+    rec = bench.link_record("all_to_all", 512 << 20, 8, [30.0, 28.0, 35.0, 29.0, 28.5, 31.0, 30.5, 29.5], "nccl")
+    assert set(rec) >= {"kind", "bytes_per_rank", "ms", "gbs_per_rank"}
+    assert rec["kind"] == "all_to_all" and rec["bytes_per_rank"] == 7 * (512 << 20)
+    assert rec["ms"] == [28.0, 35.0]
+    lo, hi = rec["gbs_per_rank"]
+    assert abs(hi - 7 * (512 << 20) / 28.0 / 1e6) < 1e-9 and lo < hi
+    assert rec["transport"] == "rccl" and "note" not in rec
+    json.dumps(rec)
+    rec = bench.link_record("all_gather", 1 << 20, 2, [5.0, 6.0], "gloo")
+    assert rec["bytes_per_rank"] == 1 << 20 and "not a link rate" in rec["note"]

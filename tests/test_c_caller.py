@@ -64,6 +64,20 @@ def test_c_caller_collective_over_rccl_api(log_n, cols, log_lde, cap, threads, l
     # bj_comm_info / bj_comm_check_world through RCCL's API: ncclCommCount = 2, 4, 8 and each
     # rank's ncclCommUserRank; the stand-in's ranks share one GPU and the check must say so
     assert "rccl world check ok at world 2 4 8" in r.stdout, r.stdout
+    assert "a failed record rejected on every rank" in r.stdout, r.stdout
+    # the link probe bench.py's N > 1 line carries ("link"): one exchange of the commit's own
+    # kind and size on every rank, at world 2, 4 and 8 (the mock's rate is a device copy's)
+    import re
+    links = re.findall(r"^link world (\d+) rank (\d+) kind (\w+) bytes_per_rank (\d+) ms ([\d.]+) gbs_per_rank ([\d.]+)$",
+                       r.stdout, re.M)
+    for world in (2, 4, 8):
+        got = [l for l in links if int(l[0]) == world]
+        assert sorted(int(l[1]) for l in got) == list(range(world)), (world, got)
+        kind = "all_to_all" if world > (1 << log_lde) else "all_gather"
+        block = 8 * (((1 << log_n) << log_k) // world) * (cols // world) * (1 << (log_lde - log_k)) \
+            if kind == "all_to_all" else 8 * (1 << log_n) * (cols // world)
+        for l in got:
+            assert l[2] == kind and int(l[3]) == (world - 1) * block and float(l[4]) > 0, (world, l)
 
 
 @pytest.mark.gpu

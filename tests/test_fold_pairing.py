@@ -5,8 +5,12 @@ Shard T's sub-coset shift is s_T = 7 w^bitrev_ls(T), w the generator of the n D 
 z_T = s_T^m.  At F = G / k = 2 the targets T and T ^ 1 are the two halves of one coset, so
 z_(T^1) = -z_T and the kernel forms both outputs as one butterfly (c0 + z c1, c0 - z c1); the host
 checks exactly this on the constants before choosing that form.  The pairing holds at every F
-(bitrev_ls(T ^ 1) differs from bitrev_ls(T) by 2^(ls-1), and w^(2^(ls-1) m) = -1), but only F = 2
-(C3 at G = 8) uses it; F = 4 and 8 keep the per-target loop.
+(bitrev_ls(T ^ 1) differs from bitrev_ls(T) by 2^(ls-1), and w^(2^(ls-1) m) = -1), and the kernel
+uses it at F = 2, 4 and 8: a butterfly at F = 2 (C3 at G = 8), E +- O at F = 4 and 8 (E the
+even-exponent terms, O the odd ones).  The per-target loop runs only under the experiment knob
+BJ_INV_FOLD_UNPAIRED=1 (with BJ_EXPERIMENTS=1), which
+tests/test_gpu_native_sharded.py::test_native_sharded_commit_env_knobs checks gives the same
+commitment.
 """
 import pytest
 
