@@ -8,9 +8,9 @@
 
 namespace bj {
 
-// Experiment knobs (round 6).  The A/B switches of the kernel schedule -- BJ_LEAVES_DEFER
-// (collective.hip), BJ_INV_FOLD_UNPAIRED (ntt_lde3.hip), BJ_LDE_PASSES (capi.hip) and
-// BJ_NODE_Q4_MAX (merkle.hip) -- are read from the environment only when BJ_EXPERIMENTS=1 is
+// Experiment knobs (round 6).  The A/B switches of the kernel schedule -- BJ_LEAVES_DEFER and
+// BJ_LEAVES_GROUP (collective.hip), BJ_INV_FOLD_UNPAIRED (ntt_lde3.hip), BJ_LDE_PASSES (capi.hip) and
+// BJ_NODE_Q4_MAX and BJ_NODE_FUSED (merkle.hip) -- are read from the environment only when BJ_EXPERIMENTS=1 is
 // set, once per process, at the first call that needs one; otherwise each has its production
 // value, so a prover's environment cannot change the schedule (the reference's
 // transform_raw_storages_to_lde, utils.rs:270-403, is a pure function of its inputs).
@@ -18,20 +18,24 @@ namespace bj {
 struct Knobs {
     bool enabled;
     uint64_t leaves_defer;       // 0: chunk k's leaves right after its own LDE
+    uint64_t leaves_group;       // 0: one chunk per leaf grid (collective.hip leaves_group())
     uint64_t inv_fold_unpaired;  // 0: the paired even/odd sender fold where the constants pair
     uint64_t lde_passes;         // 3: the three-pass LDE for 2^18..2^23 (2: head + tail per transform)
     uint64_t node_q4_max;        // 2^15: levels of at most this many digests use quad-lane permutations
+    uint64_t node_fused;         // 1: those levels run up to 8 per launch (node_levels_q4_kernel)
 };
 inline Knobs read_knobs() {
-    Knobs k{false, 0, 0, 3, (uint64_t)1 << 15};
+    Knobs k{false, 0, 0, 0, 3, (uint64_t)1 << 15, 1};
     const char* g = getenv("BJ_EXPERIMENTS");
     k.enabled = g && strcmp(g, "1") == 0;
     if (!k.enabled) return k;
     const char* e;
     if ((e = getenv("BJ_LEAVES_DEFER"))) k.leaves_defer = strtoull(e, nullptr, 0);
+    if ((e = getenv("BJ_LEAVES_GROUP"))) k.leaves_group = strtoull(e, nullptr, 0);
     if ((e = getenv("BJ_INV_FOLD_UNPAIRED"))) k.inv_fold_unpaired = e[0] == '1';
     if ((e = getenv("BJ_LDE_PASSES"))) k.lde_passes = e[0] == '2' ? 2 : 3;
     if ((e = getenv("BJ_NODE_Q4_MAX"))) k.node_q4_max = strtoull(e, nullptr, 0);
+    if ((e = getenv("BJ_NODE_FUSED"))) k.node_fused = e[0] != '0';
     return k;
 }
 // one instance per shared library (an inline function's static is merged across its TUs)

@@ -472,9 +472,11 @@ int bj_experiment_knob(const char* name, uint64_t* value) {
     const bj::Knobs& k = bj::knobs();
     if (!strcmp(name, "BJ_EXPERIMENTS")) *value = k.enabled;
     else if (!strcmp(name, "BJ_LEAVES_DEFER")) *value = k.leaves_defer;
+    else if (!strcmp(name, "BJ_LEAVES_GROUP")) *value = k.leaves_group;
     else if (!strcmp(name, "BJ_INV_FOLD_UNPAIRED")) *value = k.inv_fold_unpaired;
     else if (!strcmp(name, "BJ_LDE_PASSES")) *value = k.lde_passes;
     else if (!strcmp(name, "BJ_NODE_Q4_MAX")) *value = k.node_q4_max;
+    else if (!strcmp(name, "BJ_NODE_FUSED")) *value = k.node_fused;
     else return fail(BJ_EINVAL, std::string("bj_experiment_knob: unknown knob ") + name);
     return BJ_OK;
 }

@@ -336,6 +336,15 @@ uint32_t log2u(uint64_t x) {
 // happen on the compute stream; larger d needs the later chunks' exchanges earlier.
 size_t leaves_defer() { return (size_t)bj::knobs().leaves_defer; }
 
+// Chunks per leaf grid (BJ_LEAVES_GROUP, an experiment knob; 1 in production).  Two chunks per
+// grid halve the LDE -> leaves switches while every chunk's LDE still waits only for its own
+// arrival, but measured 0.1-0.7 ms per rank slower at C3 G = 4 and 8 with the exchange stubbed
+// (profiles/r6c_group_*.log), so each chunk keeps its own grid.
+size_t leaves_group() {
+    const uint64_t g = bj::knobs().leaves_group;
+    return g ? (size_t)g : 1;
+}
+
 struct Run {
     uint32_t lo, global, count;  // local first row, global first column, columns
     uint32_t c0, c1;             // the chunk's global column range
@@ -830,24 +839,35 @@ int bj_sharded_commit_d(bj_comm* comm, const uint64_t* trace_shard, size_t trace
     // 2. per arrived chunk: this rank's part of the committed block (block 0) of its columns'
     //    LDE, absorbed into the sponges, then its part of the other blocks (LDE only).  Chunk k's
     //    leaves follow chunk k + defer's LDE (leaves_defer(); 0 in production).
-    auto absorb = [&](size_t k) -> int {
-        const Run& r = runs[k];
-        const uint32_t cc = r.c1 - r.c0;
-        const uint64_t* out = lde + (size_t)r.c0 * m;  // block 0
-        const bool last = k + 1 == K;
-        const uint64_t* cin = k == 0 ? nullptr : state;
+    // chunks [k0, k1) in one leaf grid: their block-0 columns are contiguous (chunk k + 1's
+    // global columns follow chunk k's), so one sponge pass absorbs them
+    auto absorb = [&](size_t k0, size_t k1) -> int {
+        const uint32_t c0 = runs[k0].c0, cc = runs[k1 - 1].c1 - c0;
+        const uint64_t* out = lde + (size_t)c0 * m;  // block 0
+        const bool last = k1 == K;
+        const uint64_t* cin = k0 == 0 ? nullptr : state;
         uint64_t* dst = last ? leaves : state;
         BJ_CHECK(pt.begin(2));
         if (hasher == BJ_HASHER_POSEIDON2)
             BJ_CHECK(bj_merkle_leaves_partial_d(out, cc, m, m, cin, dst, last ? 1 : 0, st));
         else if (hasher == BJ_HASHER_BLAKE2S)
-            BJ_CHECK(bj_blake2s_leaves_partial_d(out, cc, m, m, r.c0, cin, dst, last ? 1 : 0, st));
+            BJ_CHECK(bj_blake2s_leaves_partial_d(out, cc, m, m, c0, cin, dst, last ? 1 : 0, st));
         else
             BJ_CHECK(bj_keccak256_leaves_d(out, cc, m, m, dst, st));
         return pt.end();
     };
-    const size_t defer = leaves_defer();
+    // chunk k's leaves follow chunk k + defer's LDE (leaves_defer(), 0 in production), `group`
+    // chunks per leaf grid (leaves_group(), 1 in production)
+    const size_t defer = leaves_defer(), group = leaves_group();
     size_t absorbed = 0;
+    auto absorb_ready = [&](size_t ready, bool flush) -> int {
+        while (ready > absorbed && (flush || ready - absorbed >= group)) {
+            const size_t hi = std::min(ready, absorbed + group);
+            BJ_CHECK(absorb(absorbed, hi));
+            absorbed = hi;
+        }
+        return BJ_OK;
+    };
     for (size_t k = 0; k < K; k++) {
         const Run& r = runs[k];
         const uint32_t cc = r.c1 - r.c0;
@@ -869,11 +889,10 @@ int bj_sharded_commit_d(bj_comm* comm, const uint64_t* trace_shard, size_t trace
             else
                 BJ_CHECK(bj_lde_shard_d(coeffs + (size_t)r.c0 * n, cc, n, log_n, log_lde, ls, shard, work, out, st));
             BJ_CHECK(pt.end());
-            if (j == 0)
-                while (absorbed + defer <= k) BJ_CHECK(absorb(absorbed++));
+            if (j == 0 && k + 1 > defer) BJ_CHECK(absorb_ready(k + 1 - defer, k + 1 == K));
         }
     }
-    while (absorbed < K) BJ_CHECK(absorb(absorbed++));
+    BJ_CHECK(absorb_ready(K, true));
     // 3. this rank's subtree, then the cap
     BJ_CHECK(pt.begin(3));
     BJ_CHECK(nodes_for(hasher, leaves, m, cap_local, nodes, st));

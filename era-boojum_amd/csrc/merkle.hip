@@ -215,6 +215,56 @@ __global__ __launch_bounds__(256) void node_level_q4_kernel(const uint64_t* __re
     next[4 * i + p] = ((uint64_t)z1 << 32) | z0;
 }
 
+// Levels of at most 2^15 nodes (below one wave per SIMD), several per launch (round 6): block w
+// takes the 2^b consecutive digests [w 2^b, (w + 1) 2^b) of the level below and runs `lv`
+// levels over them, one node per quad of lanes (p2q::permute), the digests between levels in
+// LDS.  Every level's nodes are stored where per-level launches would put them (levels
+// concatenated upward from `out`, node_hashes_enumerated_from_leafs; merkle_tree.rs:388-449),
+// so a block's subtree is the reference's.  One launch replaces lv per-level grids of ~17 us
+// each; the levels inside still run one permutation latency apart (a block barrier between).
+constexpr uint32_t NODE_FUSED_THREADS = 512;  // 128 quads: level 1 of a 2^8-digest block in one pass
+constexpr uint32_t NODE_FUSED_LOG_DIGESTS = 8;
+__global__ __launch_bounds__(NODE_FUSED_THREADS) void node_levels_q4_kernel(const uint64_t* __restrict__ prev,
+                                                                           uint64_t* __restrict__ out, size_t len,
+                                                                           uint32_t b, uint32_t lv) {
+    __shared__ uint64_t rcf[8 * 12];
+    __shared__ uint64_t buf[2][(NODE_FUSED_THREADS / 4) * 4];
+    const uint32_t t = threadIdx.x;
+    if (t < 8 * 12) {
+        const uint32_t r = t / 12, e = t % 12, row = r < 4 ? r : r + 22;
+        rcf[t] = p2::RCL.lo[row][e] | (p2::RCL.hi[row][e] << 32);
+    }
+    __syncthreads();
+    const uint32_t q = t >> 2, p = t & 3;
+    const p2q::Consts k = p2q::consts(p);
+    size_t base = 0, level_len = len >> 1;  // level j: level_len nodes from out + 4 base
+    uint32_t nodes = 1u << (b - 1);         // this block's nodes of level j
+    for (uint32_t j = 0; j < lv; j++) {
+        if (q < nodes) {  // whole quads (and whole waves once nodes >= 16)
+            uint64_t l, r;
+            if (j == 0) {
+                const size_t i = (size_t)blockIdx.x * nodes + q;
+                l = prev[8 * i + p];
+                r = prev[8 * i + 4 + p];
+            } else {
+                l = buf[(j - 1) & 1][8 * q + p];
+                r = buf[(j - 1) & 1][8 * q + 4 + p];
+            }
+            uint32_t lo[3] = {(uint32_t)l, (uint32_t)r, 0}, hi[3] = {(uint32_t)(l >> 32), (uint32_t)(r >> 32), 0};
+            p2q::permute(lo, hi, rcf, p, k);
+            uint32_t z0, z1;
+            glasm::canon_x1(lo[0], hi[0], z0, z1);
+            const uint64_t z = ((uint64_t)z1 << 32) | z0;
+            out[4 * (base + (size_t)blockIdx.x * nodes + q) + p] = z;
+            buf[j & 1][4 * q + p] = z;
+        }
+        __syncthreads();
+        base += level_len;
+        level_len >>= 1;
+        nodes >>= 1;
+    }
+}
+
 // Remaining levels from `len` digests (len <= 4096; launch_nodes hands over len <= 512) down to
 // cap_size, one workgroup.
 __global__ __launch_bounds__(256) void node_tail_kernel(const uint64_t* __restrict__ prev, uint64_t* next,
@@ -314,8 +364,23 @@ hipError_t launch_nodes(const uint64_t* leaves, size_t n_leaves, uint32_t cap_si
     // own grid down to the cap; BJ_NODE_Q4_MAX=0 keeps one node per lane and the one-workgroup
     // tail for the last levels.
     const size_t q4max = node_q4_max();
+    const auto pow2 = [](size_t x) { return x && !(x & (x - 1)); };
+    const bool fuse = knobs().node_fused && pow2(n_leaves) && pow2(cap_size);
     while (len > cap_size && (q4max || len > 512)) {
         size_t m = len / 2;
+        if (m <= q4max && fuse) {
+            // up to 8 levels per launch (node_levels_q4_kernel): blocks of 2^b digests
+            uint32_t L = 0, C = 0;
+            while (((size_t)1 << L) < len) L++;
+            while (((size_t)1 << C) < cap_size) C++;
+            const uint32_t b = std::min(NODE_FUSED_LOG_DIGESTS, L), lv = std::min(b, L - C);
+            hipLaunchKernelGGL(node_levels_q4_kernel, dim3((unsigned)(len >> b)), dim3(NODE_FUSED_THREADS), 0, st,
+                               prev, out, len, b, lv);
+            prev = out + 4 * (len - (len >> (lv - 1)));
+            out += 4 * (len - (len >> lv));
+            len >>= lv;
+            continue;
+        }
         if (m <= q4max)
             hipLaunchKernelGGL(node_level_q4_kernel, dim3((unsigned)((m + 63) / 64)), dim3(256), 0, st, prev, out, m);
         else

@@ -452,11 +452,13 @@ def test_local_exchange_layouts():
 
 
 @pytest.mark.parametrize("var,value", [("BJ_LEAVES_DEFER", "1"), ("BJ_LEAVES_DEFER", "99"),
-                                       ("BJ_INV_FOLD_UNPAIRED", "1")])
+                                       ("BJ_INV_FOLD_UNPAIRED", "1"), ("BJ_LEAVES_GROUP", "1"),
+                                       ("BJ_LEAVES_GROUP", "3")])
 def test_native_sharded_commit_env_knobs(torch_mod, var, value):
     """The pipeline's experiment knobs must give the same commitment: BJ_LEAVES_DEFER
     (collective.hip leaves_defer(), read once per process: chunk k's leaves after chunk k + d's
-    LDE, or after every LDE) and BJ_INV_FOLD_UNPAIRED (ntt_lde3.hip: the sender fold's
+    LDE, or after every LDE), BJ_LEAVES_GROUP (chunks per leaf grid: 1, or 3 instead of the
+    default 2) and BJ_INV_FOLD_UNPAIRED (ntt_lde3.hip: the sender fold's
     per-target loop instead of the paired even/odd form, F = 2, 4, 8).  Run in a child process."""
     import os
     import subprocess

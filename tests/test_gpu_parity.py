@@ -310,7 +310,8 @@ def test_lde_with_strided_trace(bj):
 # ------------------------------------------------------------------ Merkle
 
 @pytest.mark.parametrize("c,nl,cap", [(1, 2, 1), (5, 64, 4), (8, 1024, 16), (13, 4096, 1), (33, 1 << 13, 16),
-                                      (16, 1 << 14, 2048)])
+                                      (16, 1 << 14, 2048), (7, 1 << 9, 1), (3, 1 << 16, 256), (4, 1 << 17, 16),
+                                      (2, 1 << 18, 1)])
 def test_merkle_tree(bj, c, nl, cap):
     src = rand((c, nl), c + nl)
     t = bj.field.to_device(src)
@@ -324,10 +325,13 @@ def test_merkle_tree(bj, c, nl, cap):
         assert bj.merkle.MerkleTreeWithCap.verify_proof_over_cap(path, tree.get_cap(), leaf, idx)
 
 
-def test_node_levels_one_per_lane(bj):
+@pytest.mark.parametrize("knob,value", [("BJ_NODE_Q4_MAX", "0"), ("BJ_NODE_FUSED", "0")])
+def test_node_levels_one_per_lane(bj, knob, value):
     """BJ_NODE_Q4_MAX=0 keeps one node per lane for every level and the one-workgroup tail (the
-    form the quad kernel replaces on small levels, poseidon2_quad.hpp); both must give the
-    reference's tree.  A child process, since the library reads the variable once."""
+    form the quad kernel replaces on small levels, poseidon2_quad.hpp); BJ_NODE_FUSED=0 runs each
+    small level as its own quad-lane grid instead of up to 8 levels per launch
+    (node_levels_q4_kernel).  Every form must give the reference's tree.  A child process, since
+    the library reads the variables once (and only under BJ_EXPERIMENTS=1)."""
     import os
     import subprocess
     import sys
@@ -336,15 +340,15 @@ def test_node_levels_one_per_lane(bj):
         "from boojum_amd import field, merkle\n"
         "src = np.random.default_rng(5).integers(0, O.P, size=(9, 1 << 15), dtype=np.uint64)\n"
         "import ctypes; from boojum_amd._lib import load\n"
-        "v = ctypes.c_uint64(9); assert load().bj_experiment_knob(b'BJ_NODE_Q4_MAX', ctypes.byref(v)) == 0\n"
+        "v = ctypes.c_uint64(9); assert load().bj_experiment_knob(%r, ctypes.byref(v)) == 0\n"
         "assert v.value == 0, v.value\n"
         "for cap in (1, 16, 512):\n"
         "    tree = merkle.MerkleTreeWithCap.construct(field.to_device(src), cap)\n"
         "    leaves, nodes, levels, capr = O.merkle_construct(src, cap, threads=4)\n"
         "    assert np.array_equal(field.to_host(tree.nodes), nodes), cap\n"
         "    assert np.array_equal(tree.get_cap(), capr), cap\n"
-        "print('lane-form tree ok')\n")
-    env = dict(os.environ, BJ_EXPERIMENTS="1", BJ_NODE_Q4_MAX="0")
+        "print('lane-form tree ok')\n") % knob.encode()
+    env = dict(os.environ, BJ_EXPERIMENTS="1", **{knob: value})
     root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
     env["PYTHONPATH"] = os.pathsep.join([os.path.join(root, "era-boojum_amd"), os.path.join(root, "oracle"),
                                          env.get("PYTHONPATH", "")])

@@ -1,7 +1,7 @@
 """Experiment knobs stay out of the product path (CPU, no GPU; ABI 2.6).
 
-The library's same-binary A/B switches (BJ_LEAVES_DEFER, BJ_INV_FOLD_UNPAIRED, BJ_LDE_PASSES,
-BJ_NODE_Q4_MAX; csrc/bj_internal.hpp) are read from the environment only under BJ_EXPERIMENTS=1.
+The library's same-binary A/B switches (BJ_LEAVES_DEFER, BJ_LEAVES_GROUP, BJ_INV_FOLD_UNPAIRED, BJ_LDE_PASSES,
+BJ_NODE_Q4_MAX, BJ_NODE_FUSED; csrc/bj_internal.hpp) are read from the environment only under BJ_EXPERIMENTS=1.
 bj_experiment_knob is host-only, so a child process per environment loads the library and reads
 the values in effect: without the gate every knob keeps its production value whatever the
 environment says; with it the environment's values apply.  The reference's
@@ -16,9 +16,10 @@ import sys
 
 from test_abi import LIB
 
-PRODUCTION = {"BJ_EXPERIMENTS": 0, "BJ_LEAVES_DEFER": 0, "BJ_INV_FOLD_UNPAIRED": 0, "BJ_LDE_PASSES": 3,
-              "BJ_NODE_Q4_MAX": 1 << 15}
-SET = {"BJ_LEAVES_DEFER": "99", "BJ_INV_FOLD_UNPAIRED": "1", "BJ_LDE_PASSES": "2", "BJ_NODE_Q4_MAX": "0"}
+PRODUCTION = {"BJ_EXPERIMENTS": 0, "BJ_LEAVES_DEFER": 0, "BJ_LEAVES_GROUP": 0, "BJ_INV_FOLD_UNPAIRED": 0, "BJ_LDE_PASSES": 3,
+              "BJ_NODE_Q4_MAX": 1 << 15, "BJ_NODE_FUSED": 1}
+SET = {"BJ_LEAVES_DEFER": "99", "BJ_LEAVES_GROUP": "3", "BJ_INV_FOLD_UNPAIRED": "1", "BJ_LDE_PASSES": "2", "BJ_NODE_Q4_MAX": "0",
+       "BJ_NODE_FUSED": "0"}
 
 CODE = """
 import ctypes, json, sys
@@ -54,8 +55,8 @@ def test_knobs_ignored_without_the_gate():
 
 def test_knobs_apply_under_the_gate():
     got = knobs(dict(SET, BJ_EXPERIMENTS="1"))
-    assert got == {"BJ_EXPERIMENTS": 1, "BJ_LEAVES_DEFER": 99, "BJ_INV_FOLD_UNPAIRED": 1, "BJ_LDE_PASSES": 2,
-                   "BJ_NODE_Q4_MAX": 0, "unknown_rc": -22}
+    assert got == {"BJ_EXPERIMENTS": 1, "BJ_LEAVES_DEFER": 99, "BJ_LEAVES_GROUP": 3, "BJ_INV_FOLD_UNPAIRED": 1, "BJ_LDE_PASSES": 2,
+                   "BJ_NODE_Q4_MAX": 0, "BJ_NODE_FUSED": 0, "unknown_rc": -22}
     # BJ_INV_FOLD_UNPAIRED is parsed, not only tested for presence
     got = knobs({"BJ_EXPERIMENTS": "1", "BJ_INV_FOLD_UNPAIRED": "0"})
     assert got["BJ_INV_FOLD_UNPAIRED"] == 0
