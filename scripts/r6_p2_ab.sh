@@ -1,4 +1,4 @@
-# Round 6: the half-reduced Poseidon2 hand-off.  Parity first (permutation KATs, leaves, the
+# Round 6: a Poseidon2 change (the half-reduced hand-off, r6a; the M4 blocks, r6d).  Parity first (permutation KATs, leaves, the
 # proof.json paths, commits, the C3 golden cap), then the leaf kernel alone and the C3 commit,
 # each alternated 3x against the previous library (era-boojum_amd/boojum_amd/libboojum_mi355x.so.old,
 # tools/leaf_bench_prod_old).  usage: bash scripts/r6_p2_ab.sh TAG
