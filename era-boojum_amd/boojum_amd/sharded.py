@@ -174,21 +174,33 @@ class NativeComm:
         fn = _EXCHANGE_FN(lambda *a: 0)
         return cls._make("bj_comm_init_callback", world, rank, fn, None, 0, world=world, rank=rank, keep=fn)
 
-    def link_probe(self, kind, bytes_per_rank, stream=None):
+    def link_probe(self, kind, bytes_per_rank, stream=None, agree=None):
         """Time one bj_comm_exchange_d of `kind` (XCHG_ALL_GATHER / XCHG_ALL_TO_ALL) with
         `bytes_per_rank` bytes per rank block, as bj_sharded_commit_d's exchanges move them
         (collective; every rank calls it).  A small exchange of the same kind first sets up the
         transport's connections; the caller should hold the ranks at a barrier just before.
-        Returns the milliseconds between HIP events on `stream` around the exchange: the
-        transport's time plus any wait for peers that reached it later (so the minimum over ranks
-        is the closest to the link's own time)."""
+        `agree(ok) -> bool`, when given, is a host-side collective over the ranks (every rank's
+        buffers allocated?): the exchange runs only when every rank could allocate, so one rank's
+        allocation failure cannot leave its peers waiting in the transport.  Returns the
+        milliseconds between HIP events on `stream` around the exchange -- the transport's time
+        plus any wait for peers that reached it later, so the minimum over ranks is the closest to
+        the link's own time -- or None when a rank could not allocate."""
         dev = torch.device("cuda", torch.cuda.current_device())
         st = stream if stream is not None else torch.cuda.current_stream().cuda_stream
         world = self.world
         words = max(1, bytes_per_rank // 8)
         nsend = words * (world if kind == XCHG_ALL_TO_ALL else 1)
-        send = torch.zeros(nsend, dtype=torch.int64, device=dev)
-        recv = torch.empty(words * world, dtype=torch.int64, device=dev)
+        try:
+            send = torch.zeros(nsend, dtype=torch.int64, device=dev)
+            recv = torch.empty(words * world, dtype=torch.int64, device=dev)
+            ok = True
+        except RuntimeError:  # allocation failure: reported through agree(), never raised alone
+            send = recv = None
+            ok = False
+        if agree is not None:
+            ok = agree(ok)
+        if not ok:
+            return None
         check(load().bj_comm_exchange_d(self.handle, kind, send.data_ptr(), recv.data_ptr(), 8, st),
               "bj_comm_exchange_d")
         torch.cuda.synchronize()
