@@ -9,7 +9,7 @@
 namespace bj {
 
 // Experiment knobs (round 6).  The A/B switches of the kernel schedule -- BJ_LEAVES_DEFER and
-// BJ_LEAVES_GROUP (collective.hip), BJ_INV_FOLD_UNPAIRED (ntt_lde3.hip), BJ_LDE_PASSES (capi.hip) and
+// BJ_LEAVES_GROUP and BJ_LDE_OWN_FUSED (collective.hip), BJ_INV_FOLD_UNPAIRED (ntt_lde3.hip), BJ_LDE_PASSES (capi.hip) and
 // BJ_NODE_Q4_MAX and BJ_NODE_FUSED (merkle.hip) -- are read from the environment only when BJ_EXPERIMENTS=1 is
 // set, once per process, at the first call that needs one; otherwise each has its production
 // value, so a prover's environment cannot change the schedule (the reference's
@@ -23,9 +23,10 @@ struct Knobs {
     uint64_t lde_passes;         // 3: the three-pass LDE for 2^18..2^23 (2: head + tail per transform)
     uint64_t node_q4_max;        // 2^15: levels of at most this many digests use quad-lane permutations
     uint64_t node_fused;         // 1: those levels run up to 8 per launch (node_levels_q4_kernel)
+    uint64_t lde_own_fused;      // 1: G <= D ranks fuse their own columns' inverse tail into the forward
 };
 inline Knobs read_knobs() {
-    Knobs k{false, 0, 0, 0, 3, (uint64_t)1 << 15, 1};
+    Knobs k{false, 0, 0, 0, 3, (uint64_t)1 << 15, 1, 1};
     const char* g = getenv("BJ_EXPERIMENTS");
     k.enabled = g && strcmp(g, "1") == 0;
     if (!k.enabled) return k;
@@ -36,6 +37,7 @@ inline Knobs read_knobs() {
     if ((e = getenv("BJ_LDE_PASSES"))) k.lde_passes = e[0] == '2' ? 2 : 3;
     if ((e = getenv("BJ_NODE_Q4_MAX"))) k.node_q4_max = strtoull(e, nullptr, 0);
     if ((e = getenv("BJ_NODE_FUSED"))) k.node_fused = e[0] != '0';
+    if ((e = getenv("BJ_LDE_OWN_FUSED"))) k.lde_own_fused = e[0] != '0';
     return k;
 }
 // one instance per shared library (an inline function's static is merged across its TUs)
@@ -132,14 +134,17 @@ size_t lde3_table_len(uint32_t log_n);
 hipError_t launch_lde3_table(uint64_t* out, uint32_t log_n, uint64_t shift, hipStream_t st);
 // middle + final passes.  src: inv_tab != NULL -> the inverse head's output (natural order after
 // its log n - 13 stages), and mono (if non-NULL) receives the canonical monomials in bit-reversed
-// order; inv_tab == NULL -> src holds the monomials in bit-reversed order already.  Output coset
+// order; inv_tab == NULL -> src holds the monomials in bit-reversed order already.  `passes`
+// selects the middle pass (stages 0..12 of every coset), the final pass (the last log n - 13, in
+// place on the middle pass's output), or both.  Output coset
 // i (table tabs + i * tab_stride) of column c at lde + c * col_stride + i * coset_stride; with
 // log_k < log2(n_cosets) the cosets come in blocks of 2^log_k, coset i at
 // lde + c * col_stride + (i >> log_k) * block_stride + (i mod 2^log_k) * coset_stride.
+constexpr uint32_t LDE3_MID = 1, LDE3_FINAL = 2, LDE3_BOTH = 3;
 hipError_t launch_lde3(uint64_t* lde, size_t col_stride, size_t coset_stride, uint32_t n_cosets, const uint64_t* src,
                        size_t src_stride, uint64_t* mono, size_t mono_stride, uint32_t n_cols, uint32_t log_n,
                        const uint64_t* inv_tab, const uint64_t* tabs, size_t tab_stride, hipStream_t st,
-                       uint32_t log_k = 31, size_t block_stride = 0);
+                       uint32_t log_k = 31, size_t block_stride = 0, uint32_t passes = LDE3_BOTH);
 // the inverse tail on the inverse head's output src, folded by F = 2^log_f (1..3) for `shards`
 // targets: dst + P * dst_shard_stride + c * dst_col_stride receives column c's monomials folded
 // with s_pow_m[P] (launch_fold_all's output), the monomials themselves never written
@@ -179,6 +184,15 @@ int lde_fused_blocks(const uint64_t* trace, uint32_t n_cols, size_t trace_stride
 // T of column c at dst + T * dst_shard_stride + c * dst_col_stride, folded with s_pow_m[T] --
 // launch_fold_all's output.  inverse_fold_supported false: use bj_lde_coeffs_d + launch_fold_all.
 bool inverse_fold_supported(uint32_t log_n, uint32_t log_f, uint32_t targets);
+// capi.hip: a rank's own columns at G <= D (whole cosets [P per, (P + 1) per), per = D / G): the
+// inverse head of the trace into mono, then the inverse tail fused with forward stages 0..12 of
+// the rank's cosets (lde3_mid_kernel<R, true, true>), which writes the canonical monomials back
+// to mono (the exchange format, c_j at bitrev_n(j)) and the cosets' middle-pass output to lde
+// (column c at lde + c * col_stride, coset i at + i * 2^log_n); passes LDE3_FINAL then runs the
+// last stages in place.  The monomials are written once and never read back for these columns.
+int lde_own_shard(const uint64_t* trace, uint32_t n_cols, size_t trace_stride, uint32_t log_n, uint32_t log_lde,
+                  uint32_t log_shards, uint32_t shard, uint64_t* mono, size_t mono_stride, uint64_t* lde,
+                  size_t col_stride, uint32_t passes, hipStream_t st);
 int inverse_fold_all(const uint64_t* trace, uint32_t n_cols, size_t trace_stride, uint32_t log_n, uint32_t log_f,
                      uint32_t targets, const uint64_t* s_pow_m, uint64_t* scratch, size_t scratch_stride,
                      uint64_t* dst, size_t dst_col_stride, size_t dst_shard_stride, hipStream_t st);

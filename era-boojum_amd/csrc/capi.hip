@@ -394,6 +394,27 @@ int lde_fused_blocks(const uint64_t* trace, uint32_t n_cols, size_t trace_stride
     return BJ_OK;
 }
 
+int lde_own_shard(const uint64_t* trace, uint32_t n_cols, size_t trace_stride, uint32_t log_n, uint32_t log_lde,
+                  uint32_t log_shards, uint32_t shard, uint64_t* mono, size_t mono_stride, uint64_t* lde,
+                  size_t col_stride, uint32_t passes, hipStream_t st) {
+    if (!use_lde3(log_n) || log_shards > log_lde) return fail(BJ_EINVAL, "internal: own-shard LDE needs 2^18..2^23, G <= D");
+    if (n_cols == 0) return BJ_OK;
+    const size_t n = (size_t)1 << log_n;
+    const uint32_t per = 1u << (log_lde - log_shards);
+    const uint64_t *inv, *tabs;
+    if (int r = get_ct(log_n, true, 1, &inv)) return r;
+    if (int r = get_lde3_lde(log_n, log_lde, &tabs)) return r;
+    const size_t L = bj::lde3_table_len(log_n);
+    if (passes & bj::LDE3_MID)
+        HIP_TRY(bj::launch_ct_inverse_head(mono, mono_stride, trace, trace_stride, n_cols, log_n, inv, st), "ifft");
+    // the middle pass reads each block's 8192 words before writing its monomials back to the
+    // same words, so the head's output and the monomials share `mono`
+    HIP_TRY(bj::launch_lde3(lde, col_stride, n, per, mono, mono_stride, mono, mono_stride, n_cols, log_n, inv,
+                            tabs + (size_t)shard * per * L, L, st, 31, 0, passes),
+            "lde");
+    return BJ_OK;
+}
+
 bool inverse_fold_supported(uint32_t log_n, uint32_t log_f, uint32_t targets) {
     return use_lde3(log_n) && lde3_inv_fold_supported(log_n, log_f, targets);
 }
@@ -477,6 +498,7 @@ int bj_experiment_knob(const char* name, uint64_t* value) {
     else if (!strcmp(name, "BJ_LDE_PASSES")) *value = k.lde_passes;
     else if (!strcmp(name, "BJ_NODE_Q4_MAX")) *value = k.node_q4_max;
     else if (!strcmp(name, "BJ_NODE_FUSED")) *value = k.node_fused;
+    else if (!strcmp(name, "BJ_LDE_OWN_FUSED")) *value = k.lde_own_fused;
     else return fail(BJ_EINVAL, std::string("bj_experiment_knob: unknown knob ") + name);
     return BJ_OK;
 }

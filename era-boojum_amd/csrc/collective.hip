@@ -762,6 +762,10 @@ int bj_sharded_commit_d(bj_comm* comm, const uint64_t* trace_shard, size_t trace
     const std::vector<Run> runs = column_runs(n_cols, world, rank, hasher);
     // world 1: no exchange, so no monomials need to reach memory (one run of every column)
     const bool fused = world == 1 && runs.size() == 1 && bj::lde_fused_supported(log_n);
+    // G <= D, every coset committed: a rank's own columns of a chunk take the inverse tail fused
+    // with the forward stages 0..12 of its cosets (bj::lde_own_shard), writing the monomials for
+    // the all-gather once; only the other ranks' columns are transformed from arrived monomials
+    const bool own_fused = world > 1 && !fold && B == 1 && bj::lde_fused_supported(log_n) && bj::knobs().lde_own_fused;
     const size_t K = runs.size();
     uint32_t max_cc = 0;
     for (const Run& r : runs) max_cc = std::max(max_cc, r.c1 - r.c0);
@@ -826,7 +830,11 @@ int bj_sharded_commit_d(bj_comm* comm, const uint64_t* trace_shard, size_t trace
             if (fused) continue;  // the inverse runs inside the fused LDE (step 2)
             uint64_t* mine = coeffs + (size_t)r.global * n;
             BJ_CHECK(pt.begin(0));
-            BJ_CHECK(bj_lde_coeffs_d(tr, r.count, trace_stride, log_n, mine, n, st));
+            if (own_fused)
+                BJ_CHECK(bj::lde_own_shard(tr, r.count, trace_stride, log_n, log_lde, ls, rank, mine, n,
+                                           lde + (size_t)r.global * m, m, bj::LDE3_MID, st));
+            else
+                BJ_CHECK(bj_lde_coeffs_d(tr, r.count, trace_stride, log_n, mine, n, st));
             BJ_CHECK(pt.end());
             if (world > 1) {
                 HIP_CHECK(hipEventRecord(in.ev[k], st), "hipEventRecord");
@@ -871,6 +879,14 @@ int bj_sharded_commit_d(bj_comm* comm, const uint64_t* trace_shard, size_t trace
     for (size_t k = 0; k < K; k++) {
         const Run& r = runs[k];
         const uint32_t cc = r.c1 - r.c0;
+        if (own_fused) {
+            // the rank's own columns need no arrival: their last stages first
+            BJ_CHECK(pt.begin(1));
+            BJ_CHECK(bj::lde_own_shard(trace_shard + (size_t)r.lo * trace_stride, r.count, trace_stride, log_n,
+                                       log_lde, ls, rank, coeffs + (size_t)r.global * n, n, lde + (size_t)r.global * m,
+                                       m, bj::LDE3_FINAL, st));
+            BJ_CHECK(pt.end());
+        }
         if (world > 1) HIP_CHECK(hipStreamWaitEvent(st, arrived.ev[k], 0), "hipStreamWaitEvent");
         for (uint32_t j = 0; j < B; j++) {
             uint64_t* out = lde + ((size_t)j * n_cols + r.c0) * m;
@@ -886,7 +902,16 @@ int bj_sharded_commit_d(bj_comm* comm, const uint64_t* trace_shard, size_t trace
             } else if (fold)
                 BJ_CHECK(bj_lde_shard_folded_d(folded + ((size_t)j * n_cols + r.c0) * m, cc, m, log_n, log_lde, ls,
                                                shard, out, st));
-            else
+            else if (own_fused) {
+                // the other ranks' columns of the chunk: before and after this rank's run
+                const uint32_t before = r.global - r.c0, own_end = r.global + r.count, after = r.c1 - own_end;
+                if (before)
+                    BJ_CHECK(bj_lde_shard_d(coeffs + (size_t)r.c0 * n, before, n, log_n, log_lde, ls, shard, work, out,
+                                            st));
+                if (after)
+                    BJ_CHECK(bj_lde_shard_d(coeffs + (size_t)own_end * n, after, n, log_n, log_lde, ls, shard, work,
+                                            lde + (size_t)own_end * m, st));
+            } else
                 BJ_CHECK(bj_lde_shard_d(coeffs + (size_t)r.c0 * n, cc, n, log_n, log_lde, ls, shard, work, out, st));
             BJ_CHECK(pt.end());
             if (j == 0 && k + 1 > defer) BJ_CHECK(absorb_ready(k + 1 - defer, k + 1 == K));

@@ -736,9 +736,11 @@ __global__ void lde3_table_kernel(uint64_t* out, uint32_t log_n, uint64_t w_n, u
 template <int R>
 void launch_lde3_R(uint64_t* lde, size_t col_stride, size_t coset_stride, size_t block_stride, uint32_t log_k, uint32_t n_cosets, const uint64_t* src,
                    size_t src_stride, uint64_t* mono, size_t mono_stride, uint32_t n_cols, const uint64_t* inv_tab,
-                   const uint64_t* tabs, size_t tab_stride, hipStream_t st) {
+                   const uint64_t* tabs, size_t tab_stride, hipStream_t st, uint32_t passes) {
     const dim3 gm(n_cols << R);
-    if (inv_tab && mono)
+    if (!(passes & LDE3_MID))
+        ;
+    else if (inv_tab && mono)
         hipLaunchKernelGGL((lde3_mid_kernel<R, true, true>), gm, dim3(NT), 0, st, src, src_stride, mono, mono_stride,
                            lde, col_stride, coset_stride, block_stride, log_k, n_cols, n_cosets, inv_tab, tabs, tab_stride);
     else if (inv_tab)
@@ -748,8 +750,9 @@ void launch_lde3_R(uint64_t* lde, size_t col_stride, size_t coset_stride, size_t
         hipLaunchKernelGGL((lde3_mid_kernel<R, false, false>), gm, dim3(NT), 0, st, src, src_stride, mono,
                            mono_stride, lde, col_stride, coset_stride, block_stride, log_k, n_cols, n_cosets, inv_tab, tabs, tab_stride);
     const dim3 gf((n_cols * n_cosets) << R);
-    hipLaunchKernelGGL((lde3_final_kernel<R, 0>), gf, dim3(NT), 0, st, lde, col_stride, coset_stride, block_stride, log_k, n_cols,
-                       n_cosets, tabs, tab_stride);
+    if (passes & LDE3_FINAL)
+        hipLaunchKernelGGL((lde3_final_kernel<R, 0>), gf, dim3(NT), 0, st, lde, col_stride, coset_stride, block_stride,
+                           log_k, n_cols, n_cosets, tabs, tab_stride);
 }
 
 }  // namespace
@@ -773,7 +776,7 @@ hipError_t launch_lde3_table(uint64_t* out, uint32_t log_n, uint64_t shift, hipS
 hipError_t launch_lde3(uint64_t* lde, size_t col_stride, size_t coset_stride, uint32_t n_cosets, const uint64_t* src,
                        size_t src_stride, uint64_t* mono, size_t mono_stride, uint32_t n_cols, uint32_t log_n,
                        const uint64_t* inv_tab, const uint64_t* tabs, size_t tab_stride, hipStream_t st,
-                       uint32_t log_k, size_t block_stride) {
+                       uint32_t log_k, size_t block_stride, uint32_t passes) {
     if (n_cols == 0 || n_cosets == 0) return hipSuccess;
     if (log_k > 31) log_k = 31;
     if (!lde3_supported(log_n)) return hipErrorInvalidValue;
@@ -781,7 +784,7 @@ hipError_t launch_lde3(uint64_t* lde, size_t col_stride, size_t coset_stride, ui
     if (((uint64_t)n_cols * n_cosets) << (log_n - 13) > (0xffffffffull / NT)) return hipErrorInvalidValue;
 #define BJ_LDE3(RR)                                                                                              \
     launch_lde3_R<RR>(lde, col_stride, coset_stride, block_stride, log_k, n_cosets, src, src_stride, mono, mono_stride, n_cols, inv_tab, \
-                      tabs, tab_stride, st)
+                      tabs, tab_stride, st, passes)
     switch (log_n - 13) {
         case 5: BJ_LDE3(5); break;
         case 6: BJ_LDE3(6); break;

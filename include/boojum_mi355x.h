@@ -52,7 +52,7 @@ uint32_t bj_abi_version(void);
 /* The value in effect of one experiment knob (ABI 2.6; no reference counterpart).  The library's
  * same-binary A/B switches -- BJ_LEAVES_DEFER (default 0), BJ_LEAVES_GROUP (0: one chunk per
  * leaf grid), BJ_INV_FOLD_UNPAIRED (0),
- * BJ_LDE_PASSES (3), BJ_NODE_Q4_MAX (32768) and BJ_NODE_FUSED (1) -- are read from the environment only when
+ * BJ_LDE_PASSES (3), BJ_NODE_Q4_MAX (32768), BJ_NODE_FUSED (1) and BJ_LDE_OWN_FUSED (1) -- are read from the environment only when
  * BJ_EXPERIMENTS=1 is set, once per process at the first call that needs one; otherwise each
  * keeps its production value, so a prover's environment cannot change the kernel schedule (the
  * reference's transform_raw_storages_to_lde, cs/implementations/utils.rs:270-403, is a pure

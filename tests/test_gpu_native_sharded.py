@@ -165,6 +165,12 @@ def run_local(torch, world, n_cols, log_n, log_lde, cap, hasher, log_k=None):
     (4, (16, 18, 2, 16, "poseidon2")),        # one coset per rank
     (4, (16, 19, 3, 32, "blake2s")),          # two cosets per rank
     (2, (16, 18, 3, 32, "poseidon2", 1)),     # G = k < D, B = 4
+    # G <= D, every coset committed: a rank's own columns take the inverse tail fused with its
+    # cosets' forward stages (bj::lde_own_shard), the others' columns come from the gathered
+    # monomials on both sides of the own run
+    (4, (12, 18, 2, 16, "poseidon2")),        # 3 columns per rank: one chunk, own run in the middle
+    (8, (16, 18, 3, 32, "poseidon2")),        # G = D = 8: one coset per rank
+    (2, (24, 19, 3, 16, "blake2s")),          # four cosets per rank, chaining value across chunks
 ])
 def test_native_sharded_commit_local_ranks(torch_mod, world, cfg):
     n_cols, log_n, log_lde, cap, hasher = cfg[:5]
@@ -453,12 +459,13 @@ def test_local_exchange_layouts():
 
 @pytest.mark.parametrize("var,value", [("BJ_LEAVES_DEFER", "1"), ("BJ_LEAVES_DEFER", "99"),
                                        ("BJ_INV_FOLD_UNPAIRED", "1"), ("BJ_LEAVES_GROUP", "1"),
-                                       ("BJ_LEAVES_GROUP", "3")])
+                                       ("BJ_LEAVES_GROUP", "3"), ("BJ_LDE_OWN_FUSED", "0")])
 def test_native_sharded_commit_env_knobs(torch_mod, var, value):
     """The pipeline's experiment knobs must give the same commitment: BJ_LEAVES_DEFER
     (collective.hip leaves_defer(), read once per process: chunk k's leaves after chunk k + d's
     LDE, or after every LDE), BJ_LEAVES_GROUP (chunks per leaf grid: 1, or 3 instead of the
-    default 2) and BJ_INV_FOLD_UNPAIRED (ntt_lde3.hip: the sender fold's
+    default 1), BJ_LDE_OWN_FUSED=0 (G <= D: every column's forward from the gathered monomials
+    instead of the own columns' inverse tail fused with their forward) and BJ_INV_FOLD_UNPAIRED (ntt_lde3.hip: the sender fold's
     per-target loop instead of the paired even/odd form, F = 2, 4, 8).  Run in a child process."""
     import os
     import subprocess

@@ -17,9 +17,9 @@ import sys
 from test_abi import LIB
 
 PRODUCTION = {"BJ_EXPERIMENTS": 0, "BJ_LEAVES_DEFER": 0, "BJ_LEAVES_GROUP": 0, "BJ_INV_FOLD_UNPAIRED": 0, "BJ_LDE_PASSES": 3,
-              "BJ_NODE_Q4_MAX": 1 << 15, "BJ_NODE_FUSED": 1}
+              "BJ_NODE_Q4_MAX": 1 << 15, "BJ_NODE_FUSED": 1, "BJ_LDE_OWN_FUSED": 1}
 SET = {"BJ_LEAVES_DEFER": "99", "BJ_LEAVES_GROUP": "3", "BJ_INV_FOLD_UNPAIRED": "1", "BJ_LDE_PASSES": "2", "BJ_NODE_Q4_MAX": "0",
-       "BJ_NODE_FUSED": "0"}
+       "BJ_NODE_FUSED": "0", "BJ_LDE_OWN_FUSED": "0"}
 
 CODE = """
 import ctypes, json, sys
@@ -56,7 +56,7 @@ def test_knobs_ignored_without_the_gate():
 def test_knobs_apply_under_the_gate():
     got = knobs(dict(SET, BJ_EXPERIMENTS="1"))
     assert got == {"BJ_EXPERIMENTS": 1, "BJ_LEAVES_DEFER": 99, "BJ_LEAVES_GROUP": 3, "BJ_INV_FOLD_UNPAIRED": 1, "BJ_LDE_PASSES": 2,
-                   "BJ_NODE_Q4_MAX": 0, "BJ_NODE_FUSED": 0, "unknown_rc": -22}
+                   "BJ_NODE_Q4_MAX": 0, "BJ_NODE_FUSED": 0, "BJ_LDE_OWN_FUSED": 0, "unknown_rc": -22}
     # BJ_INV_FOLD_UNPAIRED is parsed, not only tested for presence
     got = knobs({"BJ_EXPERIMENTS": "1", "BJ_INV_FOLD_UNPAIRED": "0"})
     assert got["BJ_INV_FOLD_UNPAIRED"] == 0
