@@ -331,9 +331,10 @@ uint32_t log2u(uint64_t x) {
     return l;
 }
 
-// BJ_LEAVES_DEFER=d (an experiment knob, bj_internal.hpp; tools/shard_compute_probe.py): chunk k's leaves are issued
-// after chunk k + d's LDE instead of right after its own (d = 0), so fewer LDE -> leaf switches
-// happen on the compute stream; larger d needs the later chunks' exchanges earlier.
+// BJ_LEAVES_DEFER=d (an experiment knob, bj_internal.hpp; tools/shard_compute_probe.py): chunk
+// k's leaves are issued after chunk k + d's LDE instead of right after its own (d = 0), so fewer
+// LDE -> leaf switches happen on the compute stream; larger d needs the later chunks' exchanges
+// earlier.
 size_t leaves_defer() { return (size_t)bj::knobs().leaves_defer; }
 
 // Chunks per leaf grid (BJ_LEAVES_GROUP, an experiment knob; 1 in production).  Two chunks per
@@ -668,7 +669,7 @@ int bj_comm_check_world(bj_comm* c, bj_comm_info_t* all_out, void* stream) {
             return err(BJ_EINVAL, "bj_comm_check_world: rank " + std::to_string(all_out[p].rank) +
                                       " could not read its transport record (code " +
                                       std::to_string(all_out[p].reserved[0]) + ")" +
-                                      (info_err.empty() ? std::string() : ": " + info_err));
+                                      (p == c->rank && !info_err.empty() ? ": " + info_err : std::string()));
     // what the transport saw: every rank in its own slot, the transport's count and rank equal to
     // the communicator's; an RCCL world with one device per rank (the local and callback
     // transports may share a device by design: ranks as threads, a rehearsal over gloo)
@@ -765,7 +766,8 @@ int bj_sharded_commit_d(bj_comm* comm, const uint64_t* trace_shard, size_t trace
     // G <= D, every coset committed: a rank's own columns of a chunk take the inverse tail fused
     // with the forward stages 0..12 of its cosets (bj::lde_own_shard), writing the monomials for
     // the all-gather once; only the other ranks' columns are transformed from arrived monomials
-    const bool own_fused = world > 1 && !fold && B == 1 && bj::lde_fused_supported(log_n) && bj::knobs().lde_own_fused;
+    const bool own_fused =
+        world > 1 && !fold && B == 1 && bj::lde_fused_supported(log_n) && bj::knobs().lde_own_fused;
     const size_t K = runs.size();
     uint32_t max_cc = 0;
     for (const Run& r : runs) max_cc = std::max(max_cc, r.c1 - r.c0);
