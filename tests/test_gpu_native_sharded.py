@@ -171,6 +171,7 @@ def run_local(torch, world, n_cols, log_n, log_lde, cap, hasher, log_k=None):
     (4, (12, 18, 2, 16, "poseidon2")),        # 3 columns per rank: one chunk, own run in the middle
     (8, (16, 18, 3, 32, "poseidon2")),        # G = D = 8: one coset per rank
     (2, (24, 19, 3, 16, "blake2s")),          # four cosets per rank, chaining value across chunks
+    (2, (16, 18, 2, 16, "keccak256")),        # no continuation: one chunk, own run then the peer's
 ])
 def test_native_sharded_commit_local_ranks(torch_mod, world, cfg):
     n_cols, log_n, log_lde, cap, hasher = cfg[:5]
